@@ -1,0 +1,138 @@
+/*
+ * ppgpu.h — C ABI of libppgpu.so, the MI355X (gfx950) replacement for the native layer under
+ * Quantumzhao/ParallelParsing's chunked-gzip DecompressAll path.
+ *
+ * The reference reaches native code only through Interop/PlatformInterop.cs:6-35
+ * ([DllImport("libz")] inflateInit2_/inflatePrime/inflateSetDictionary/inflate/inflateEnd/
+ * inflateReset, driven by Decompressor/Core.cs).  This ABI replaces that layer one level up:
+ * a C# host keeps Core/IndexIO/BatchedFASTQ's API surface and binds these entry points with a
+ * [DllImport("ppgpu")] class of the same shape as LibZ (INTEGRATION.md shows the stub).
+ *
+ * Conventions (mirroring Interop/Conventions.cs):
+ *  - every entry point returns an int status: PPG_OK (0) or a negative code; the ZResult values
+ *    (Conventions.cs:9-20) keep their meaning, device failures get their own codes;
+ *  - no exceptions cross the ABI; caller-owned buffers are pinned by the caller (as Core.cs:162,
+ *    171 pins Memory<byte>) and never retained; library-owned objects have explicit _free/_close;
+ *  - one ppg_ctx per GPU; a ctx is used by one host thread at a time (the reference's
+ *    per-call ZStream, Core.cs:136, is likewise single-threaded).
+ */
+#ifndef PPGPU_H
+#define PPGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: ZResult (Interop/Conventions.cs:9-20) + library codes ---- */
+#define PPG_OK 0
+#define PPG_STREAM_END 1
+#define PPG_NEED_DICT 2
+#define PPG_ERRNO (-1)
+#define PPG_STREAM_ERROR (-2)
+#define PPG_DATA_ERROR (-3)
+#define PPG_MEM_ERROR (-4)
+#define PPG_BUF_ERROR (-5)
+#define PPG_VERSION_ERROR (-6)
+#define PPG_INDEX_OUT_OF_RANGE (-50) /* C# IndexOutOfRangeException (>32 KiB without '@') */
+#define PPG_IO_ERROR (-51)
+#define PPG_ARG_ERROR (-52)
+#define PPG_DEVICE_ERROR (-100)
+#define PPG_NO_DEVICE (-101)
+
+#define PPG_WINSIZE 32768 /* Common/Constants.cs:9  */
+#define PPG_CHUNK 16384   /* Common/Constants.cs:12 */
+
+/* ======================= Index (Common/Index.cs, Common/IndexIO.cs) ======================= */
+typedef struct ppg_index ppg_index;
+
+/* CreateIndex: Core.BuildDeflateIndex(FileStream, uint chunksize) — Decompressor/Core.cs:14-131.
+ * Host-side (serial zlib pass, as in the reference).  _mem takes the whole .gz in memory. */
+int ppg_index_build_file(const char *gz_path, uint32_t chunksize, ppg_index **out);
+int ppg_index_build_mem(const uint8_t *gz, int64_t gz_len, uint32_t chunksize, ppg_index **out);
+
+/* Serialize / Deserialize — Common/IndexIO.cs:7-27 / :29-53 (byte-identical .gzi format). */
+int ppg_index_serialize(const ppg_index *ix, const char *path);
+int ppg_index_deserialize(const char *path, ppg_index **out);
+
+/* Build an Index from caller arrays (the form a C# host holding an Index would pass; Point
+ * fields of Common/Index.cs:51-82).  windows: count*32768 bytes; offsets concatenated with
+ * offset_len[i] bytes each. */
+int ppg_index_from_points(int32_t count, const int64_t *output, const int64_t *input, const int32_t *bits,
+                          const uint8_t *windows, const int32_t *offset_len, const uint8_t *offsets,
+                          int32_t chunk_max_bytes, ppg_index **out);
+
+int32_t ppg_index_count(const ppg_index *ix);                 /* Index.Count (Index.cs:21) */
+int32_t ppg_index_chunk_max_bytes(const ppg_index *ix);       /* Index.ChunkMaxBytes (Index.cs:10) */
+int ppg_index_point(const ppg_index *ix, int32_t i, int64_t *output, int64_t *input, int32_t *bits,
+                    int32_t *offset_len);                     /* Index[i] (Index.cs:20) */
+const uint8_t *ppg_index_window(const ppg_index *ix, int32_t i);  /* Point.Window */
+const uint8_t *ppg_index_offset(const ppg_index *ix, int32_t i);  /* Point.offset */
+void ppg_index_free(ppg_index *ix);
+
+/* ================================= device context ================================= */
+typedef struct ppg_ctx ppg_ctx;
+
+int ppg_device_count(int *n);
+int ppg_open(int device, ppg_ctx **out);
+void ppg_close(ppg_ctx *ctx);
+void *ppg_ctx_stream(ppg_ctx *ctx); /* the hipStream_t every kernel of this ctx runs on */
+
+/* ====================== Decompress one checkpoint (README "Decompress") ======================
+ * Core.ExtractDeflateIndex(fileBuffer, from=Index[k], to=Index[k+1], buf) — Core.cs:133-192,
+ * plus Parsing.Parse of offset_k ++ chunk (BatchedFASTQ.cs:67-68).  `slice` holds file bytes
+ * [Index[k].Input-1, Index[k+1].Input-1] exactly as LazyFileReader reads them
+ * (LazyFileReader.cs:63-69).  out receives to.Output-from.Output bytes; `produced` the count
+ * (Core.cs:191).  If recs is non-NULL, up to rec_cap records are written as 4 uint32 newline
+ * positions (n1..n4) relative to raw = offset_k ++ out; *nrec gets the record count. */
+int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
+                         uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
+                         int64_t *nrec);
+
+/* ======================= DecompressAll over a shard (README "DecompressAll") =======================
+ * A shard is chunks [first, first+n) of an index, with their compressed bytes resident on the
+ * ctx's GPU: comp holds file bytes [Index[first].Input-1, Index[first+n].Input-1]
+ * (comp_len = Index[first+n].Input - Index[first].Input + 1).  comp_on_device != 0 means comp
+ * is already a device pointer on this GPU (4-byte aligned, readable 64 bytes past comp_len);
+ * otherwise it is copied.  out_capacity bounds the device output buffer: chunks are decoded
+ * in batches whose outputs fit, the buffer being reused (0 = whole shard at once). */
+typedef struct ppg_shard ppg_shard;
+
+int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n, const void *comp, int64_t comp_len,
+                     int comp_on_device, int64_t out_capacity, ppg_shard **out);
+void ppg_shard_free(ppg_shard *sh);
+
+/* Inflate + parse every chunk of the shard (BatchedFASTQ's populateCache body, BatchedFASTQ.cs:
+ * 63-74, for all chunks).  Returns 0, or the first chunk error (ZResult code).  Blocking. */
+int ppg_shard_run(ppg_shard *sh);
+
+/* Per-chunk results of the last run (host arrays of length n; any may be NULL). */
+int ppg_shard_results(ppg_shard *sh, int64_t *records, int64_t *produced, int32_t *status, int32_t *flags,
+                      int64_t *end_bit);
+int64_t ppg_shard_total_records(ppg_shard *sh);
+int32_t ppg_shard_batches(ppg_shard *sh);
+
+/* Valid only when the shard ran as one batch: chunk bytes / record descriptors to the host.
+ * Descriptor j of chunk k = 4 uint32 (n1,n2,n3,n4) relative to raw_k = offset_k ++ chunk_k:
+ * Identifier=[r+1,n1) Sequence=[n1+1,n2) Other=[n2+2,n3) Quality=[n3+1,n4), where r = 0 for
+ * the chunk's first record and the previous n4+1 otherwise (Parsing.cs:11-51). */
+int ppg_shard_copy_chunk(ppg_shard *sh, int32_t k, uint8_t *dst, int64_t cap, int64_t *len);
+int ppg_shard_copy_records(ppg_shard *sh, int32_t k, uint32_t *dst, int64_t cap, int64_t *nrec);
+int ppg_shard_record_base(ppg_shard *sh, int64_t *base); /* n record bases (exclusive scan) */
+
+/* Device-resident per-chunk record counts (int64[n]) copied to caller device memory on this
+ * GPU (the input of the cross-GPU all-gather). */
+int ppg_shard_counts_to_device(ppg_shard *sh, int64_t *dev_dst);
+
+/* Device time of the last run, from hipEvents on the ctx stream: inflate kernels only, parse
+ * kernels only, and the whole run (ms). */
+int ppg_shard_timing(ppg_shard *sh, float *inflate_ms, float *parse_ms, float *total_ms);
+
+/* Library build string (kernel ISA, version). */
+const char *ppg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPGPU_H */

@@ -1,0 +1,374 @@
+"""parallelparsing_amd — MI355X-native chunked-gzip FASTQ DecompressAll.
+
+Host-side mirror of the reference's API surface (names, argument meaning, error behaviour) over
+the C ABI of libppgpu.so (include/ppgpu.h):
+
+  Core.BuildDeflateIndex(path_or_bytes, chunksize)        Decompressor/Core.cs:14-131 (CreateIndex)
+  Core.ExtractDeflateIndex(file_buffer, index, k, buf)     Decompressor/Core.cs:133-192 (Decompress)
+  Parsing.Parse(chunk)                                     Decompressor/Parsing.cs:11-51
+  IndexIO.Serialize(index, path) / IndexIO.Deserialize    Common/IndexIO.cs:7-53
+  BatchedFASTQ(index_or_path, gzip_path, ssd)              Decompressor/BatchedFASTQ.cs:10-101 (DecompressAll)
+  FastqRecord / Index / Point                              Common/FastqRecord.cs, Common/Index.cs
+
+Errors raise PpgError (the ZException of Interop/Conventions.cs:33-41) carrying the ZResult code.
+The decode runs only on the GPU; there is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._lib import lib, check, PpgError, PPG_NO_DEVICE, synth  # noqa: F401
+
+WINSIZE = 32768
+CHUNK = 16384
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Point:
+    """Common/Index.cs:51-82 (read-only view)."""
+
+    __slots__ = ("Output", "Input", "Bits", "Window", "offset")
+
+    def __init__(self, output, inp, bits, window, offset):
+        self.Output, self.Input, self.Bits, self.Window, self.offset = output, inp, bits, window, offset
+
+    def __repr__(self):
+        return f"Point(Output={self.Output}, Input={self.Input}, Bits={self.Bits}, |offset|={len(self.offset)})"
+
+
+class Index:
+    """Common/Index.cs: the checkpoint list, owned by libppgpu (ppg_index)."""
+
+    def __init__(self, handle):
+        self._h = C.c_void_p(handle)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.ppg_index_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def Count(self):
+        return lib.ppg_index_count(self._h)
+
+    def __len__(self):
+        return self.Count
+
+    @property
+    def ChunkMaxBytes(self):
+        return lib.ppg_index_chunk_max_bytes(self._h)
+
+    def point_fields(self, i):
+        o, n, b, ol = C.c_int64(), C.c_int64(), C.c_int32(), C.c_int32()
+        check(lib.ppg_index_point(self._h, i, C.byref(o), C.byref(n), C.byref(b), C.byref(ol)), "Index[i]")
+        return o.value, n.value, b.value, ol.value
+
+    def __getitem__(self, i):
+        if i < 0:
+            i += self.Count
+        o, n, b, ol = self.point_fields(i)
+        w = C.string_at(lib.ppg_index_window(self._h, i), WINSIZE)
+        off = C.string_at(lib.ppg_index_offset(self._h, i), ol) if ol else b""
+        return Point(o, n, b, w, off)
+
+    def arrays(self):
+        """(output, input, bits) int64 numpy arrays over all points."""
+        n = self.Count
+        out = np.empty(n, np.int64)
+        inp = np.empty(n, np.int64)
+        bits = np.empty(n, np.int64)
+        for i in range(n):
+            out[i], inp[i], bits[i], _ = self.point_fields(i)
+        return out, inp, bits
+
+    @staticmethod
+    def from_points(output, inp, bits, windows, offset_len, offsets, chunk_max_bytes=0):
+        """Index from arrays (ppg_index_from_points): windows is count*32768 bytes."""
+        output = np.ascontiguousarray(output, np.int64)
+        inp = np.ascontiguousarray(inp, np.int64)
+        bits = np.ascontiguousarray(bits, np.int32)
+        windows = np.ascontiguousarray(windows, np.uint8)
+        offset_len = np.ascontiguousarray(offset_len, np.int32)
+        offsets = np.ascontiguousarray(offsets, np.uint8) if len(offsets) else np.zeros(1, np.uint8)
+        h = C.c_void_p()
+        check(lib.ppg_index_from_points(len(output), _ptr(output), _ptr(inp), _ptr(bits), _ptr(windows),
+                                        _ptr(offset_len), _ptr(offsets), int(chunk_max_bytes), C.byref(h)),
+              "Index.from_points")
+        return Index(h.value)
+
+
+class IndexIO:
+    """Common/IndexIO.cs."""
+
+    @staticmethod
+    def Serialize(index, path):
+        check(lib.ppg_index_serialize(index.handle, os.fsencode(path)), "IndexIO.Serialize")
+
+    @staticmethod
+    def Deserialize(path):
+        h = C.c_void_p()
+        check(lib.ppg_index_deserialize(os.fsencode(path), C.byref(h)), "IndexIO.Deserialize")
+        return Index(h.value)
+
+
+class Device:
+    """One GPU context (ppg_ctx): a HIP stream on an MI355X."""
+
+    _default = {}
+
+    def __init__(self, device=0):
+        h = C.c_void_p()
+        check(lib.ppg_open(int(device), C.byref(h)), f"ppg_open({device})")
+        self._h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.ppg_close(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self):
+        return lib.ppg_ctx_stream(self._h)
+
+    @classmethod
+    def default(cls, device=None):
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        if device not in cls._default:
+            cls._default[device] = cls(device)
+        return cls._default[device]
+
+
+def device_count():
+    n = C.c_int(0)
+    lib.ppg_device_count(C.byref(n))
+    return n.value
+
+
+class FastqRecord:
+    """Common/FastqRecord.cs: Identifier, Sequence, Other, Quality (bytes fields, lazy str)."""
+
+    __slots__ = ("raw", "start", "n1", "n2", "n3", "n4")
+
+    def __init__(self, raw, start, n1, n2, n3, n4):
+        self.raw, self.start, self.n1, self.n2, self.n3, self.n4 = raw, start, n1, n2, n3, n4
+
+    # field slices exactly as Parsing.cs:37-40
+    @property
+    def identifier(self):
+        return bytes(self.raw[self.start + 1:self.n1])
+
+    @property
+    def sequence(self):
+        return bytes(self.raw[self.n1 + 1:self.n2])
+
+    @property
+    def other(self):
+        return bytes(self.raw[self.n2 + 2:self.n3])
+
+    @property
+    def quality(self):
+        return bytes(self.raw[self.n3 + 1:self.n4])
+
+    Identifier = property(lambda s: s.identifier.decode("ascii", "replace"))
+    Sequence = property(lambda s: s.sequence.decode("ascii", "replace"))
+    Other = property(lambda s: s.other.decode("ascii", "replace"))
+    Quality = property(lambda s: s.quality.decode("ascii", "replace"))
+
+    def __repr__(self):
+        return f"FastqRecord({self.identifier!r})"
+
+
+def records_from_descriptors(raw, desc):
+    """FastqRecords of one chunk from its (n,4) uint32 descriptors over raw = offset ++ chunk."""
+    recs = []
+    start = 0
+    for n1, n2, n3, n4 in np.asarray(desc).reshape(-1, 4).tolist():
+        recs.append(FastqRecord(raw, start, n1, n2, n3, n4))
+        start = n4 + 1
+    return recs
+
+
+class Parsing:
+    """Decompressor/Parsing.cs — the GPU record scan runs inside Core/Shard; this helper rebuilds
+    FastqRecord objects from its descriptors."""
+
+    @staticmethod
+    def Parse(offset, chunk, desc):
+        raw = bytes(offset or b"") + bytes(chunk)
+        return records_from_descriptors(raw, desc)
+
+
+def _as_u8(buf):
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf, np.uint8)
+    return np.frombuffer(bytes(buf), np.uint8)
+
+
+class Core:
+    """Decompressor/Core.cs."""
+
+    @staticmethod
+    def BuildDeflateIndex(gz, chunksize):
+        """CreateIndex over a path or in-memory .gz bytes (Core.cs:14-131)."""
+        h = C.c_void_p()
+        if isinstance(gz, (str, os.PathLike)):
+            check(lib.ppg_index_build_file(os.fsencode(gz), int(chunksize) & 0xFFFFFFFF, C.byref(h)),
+                  "Core.BuildDeflateIndex")
+        else:
+            a = _as_u8(gz)
+            check(lib.ppg_index_build_mem(_ptr(a), a.size, int(chunksize) & 0xFFFFFFFF, C.byref(h)),
+                  "Core.BuildDeflateIndex")
+        return Index(h.value)
+
+    @staticmethod
+    def ExtractDeflateIndex(file_buffer, index, k, buf=None, device=None, with_records=False):
+        """Decompress checkpoint k (Core.cs:133-192) on the GPU.  file_buffer = file bytes
+        [Index[k].Input-1, Index[k+1].Input-1].  Returns the produced byte count written into buf
+        (allocated if None) — and the (n,4) record descriptors if with_records."""
+        dev = device or Device.default()
+        src = _as_u8(file_buffer)
+        o0, _, _, _ = index.point_fields(k)
+        o1, _, _, _ = index.point_fields(k + 1)
+        need = max(0, o1 - o0)
+        if buf is None:
+            buf = np.zeros(need, np.uint8)
+        produced = C.c_int64()
+        nrec = C.c_int64()
+        recs = np.zeros((max(1, need // 4 + 1), 4), np.uint32) if with_records else None
+        check(lib.ppg_decompress_chunk(dev.handle, index.handle, int(k), _ptr(src), src.size, _ptr(buf), buf.size,
+                                       C.byref(produced), _ptr(recs), recs.shape[0] if with_records else 0,
+                                       C.byref(nrec)), "Core.ExtractDeflateIndex")
+        if with_records:
+            return produced.value, buf, recs[:nrec.value]
+        return produced.value, buf
+
+
+class Shard:
+    """DecompressAll over index chunks [first, first+n) resident on one GPU (ppg_shard)."""
+
+    def __init__(self, index, comp, first=0, n=None, device=None, comp_on_device=False, comp_len=None,
+                 out_capacity=0):
+        self.index = index
+        self.dev = device or Device.default()
+        if n is None:
+            n = index.Count - 1 - first
+        self.first, self.n = first, n
+        if comp_on_device:
+            ptr, length = int(comp), int(comp_len)
+        else:
+            self._host = _as_u8(comp)
+            ptr, length = self._host.ctypes.data, self._host.size
+        h = C.c_void_p()
+        check(lib.ppg_shard_create(self.dev.handle, index.handle, first, n, C.c_void_p(ptr), length,
+                                   1 if comp_on_device else 0, int(out_capacity), C.byref(h)), "ppg_shard_create")
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.ppg_shard_free(h)
+            self._h = None
+
+    def run(self):
+        check(lib.ppg_shard_run(self._h), "DecompressAll")
+        return self
+
+    @property
+    def batches(self):
+        return lib.ppg_shard_batches(self._h)
+
+    def results(self):
+        n = self.n
+        rec, prod, end = (np.zeros(n, np.int64) for _ in range(3))
+        st, fl = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        check(lib.ppg_shard_results(self._h, _ptr(rec), _ptr(prod), _ptr(st), _ptr(fl), _ptr(end)), "results")
+        return {"records": rec, "produced": prod, "status": st, "flags": fl, "end_bit": end}
+
+    @property
+    def total_records(self):
+        return lib.ppg_shard_total_records(self._h)
+
+    def chunk_bytes(self, k):
+        o0, _, _, _ = self.index.point_fields(self.first + k)
+        o1, _, _, _ = self.index.point_fields(self.first + k + 1)
+        dst = np.zeros(max(1, o1 - o0), np.uint8)
+        ln = C.c_int64()
+        check(lib.ppg_shard_copy_chunk(self._h, k, _ptr(dst), dst.size, C.byref(ln)), "copy_chunk")
+        return dst[:ln.value]
+
+    def chunk_records(self, k):
+        nrec = C.c_int64()
+        check(lib.ppg_shard_copy_records(self._h, k, None, 0, C.byref(nrec)), "copy_records")
+        dst = np.zeros((max(1, nrec.value), 4), np.uint32)
+        check(lib.ppg_shard_copy_records(self._h, k, _ptr(dst), dst.shape[0], C.byref(nrec)), "copy_records")
+        return dst[:nrec.value]
+
+    def record_base(self):
+        b = np.zeros(self.n, np.int64)
+        check(lib.ppg_shard_record_base(self._h, _ptr(b)), "record_base")
+        return b
+
+    def counts_to_device(self, dev_ptr):
+        check(lib.ppg_shard_counts_to_device(self._h, C.c_void_p(int(dev_ptr))), "counts_to_device")
+
+    def timing(self):
+        a, b, c = C.c_float(), C.c_float(), C.c_float()
+        check(lib.ppg_shard_timing(self._h, C.byref(a), C.byref(b), C.byref(c)), "timing")
+        return {"inflate_ms": a.value, "parse_ms": b.value, "total_ms": c.value}
+
+
+class BatchedFASTQ:
+    """Decompressor/BatchedFASTQ.cs:10-101 — DecompressAll as an iterable of FastqRecord.
+
+    The reference yields records in a nondeterministic interleaving; this yields the
+    canonical order: chunk 0's records, then chunk 1's, ...  enable_ssd_optimization is accepted
+    for signature parity (it selected 1 or 8 FileStreams, LazyFileReader.cs:27-33)."""
+
+    def __init__(self, index, gzip_path, enable_ssd_optimization=False, device=None):
+        if isinstance(index, (str, os.PathLike)):
+            index = IndexIO.Deserialize(index)
+        self.index = index
+        self.gzip_path = gzip_path
+        self.enable_ssd_optimization = enable_ssd_optimization
+        self.dev = device
+        self._shard = None
+
+    def _run(self):
+        if self._shard is None:
+            n = self.index.Count - 1
+            _, i0, _, _ = self.index.point_fields(0)
+            _, i1, _, _ = self.index.point_fields(n)
+            with open(self.gzip_path, "rb") as f:
+                f.seek(i0 - 1)
+                comp = f.read(i1 - i0 + 1)
+            self._shard = Shard(self.index, comp, 0, n, device=self.dev).run()
+        return self._shard
+
+    def Count(self):
+        return self._run().total_records
+
+    def __iter__(self):
+        sh = self._run()
+        for k in range(sh.n):
+            off = self.index[k].offset
+            raw = bytes(off) + sh.chunk_bytes(k).tobytes()
+            yield from records_from_descriptors(raw, sh.chunk_records(k))
+
+    def Dispose(self):
+        self._shard = None

@@ -1,0 +1,379 @@
+// synth.cpp — synthetic inputs for tests and bench.py (host only; NOT the hot path).
+//
+// Record shape follows Generator/Generator.cs:9-61 with the read length fixed (150 in
+// BASELINE.json):  "@SRR{id}.{major}.{minor} {major} length={L}\n" + L bases from ACGT +
+// "+SRR{id2}.{major}.{minor} {major} length={L}\n" + L quality chars ('?' .90, '*' .05,
+// '!' .05).  id ~ U[10^7, 2*10^7), major = no/2+1, minor = no%2+1 (Generator.cs:36-43).
+// The RNG is counter-based (record number -> stream), so any record range can be generated
+// independently and in parallel; it is not .NET's Random(0) (unreproducible without .NET).
+//
+// Compression produces ONE gzip member (the reference cannot read multi-member files, SURVEY
+// Q3).  For large inputs it is pigz-style: pieces compressed in parallel, each primed with the
+// previous piece's last 32 KiB and closed by Z_SYNC_FLUSH, CRCs joined with crc32_combine.
+//
+// The 50 GB bench file is a "tiled" member: a segment S of whole records is deflated with no
+// history (its first piece has no dictionary) and ends byte-aligned, so the same compressed
+// segment bytes can be repeated T times inside one member; the decompressed stream is S^T.
+// ppg_synth_tiled_points() derives that file's CreateIndex points (Core.cs:14-131 semantics)
+// from the segment's deflate block list without inflating the 50 GB.
+#include <zlib.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <stdio.h>
+#include <thread>
+#include <vector>
+#include <atomic>
+#include <algorithm>
+
+namespace {
+
+inline uint64_t splitmix(uint64_t &s) {
+    s += 0x9E3779B97F4A7C15ull;
+    uint64_t z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+inline int put_u(char *p, uint64_t v) {
+    char tmp[24];
+    int n = 0;
+    do { tmp[n++] = char('0' + v % 10); v /= 10; } while (v);
+    for (int i = 0; i < n; i++) p[i] = tmp[n - 1 - i];
+    return n;
+}
+
+inline int digits(uint64_t v) { int n = 1; while (v >= 10) { v /= 10; n++; } return n; }
+
+// bytes of record `no` (independent of the random draws: ids always have 8 digits)
+inline int64_t rec_size(int64_t no, int L) {
+    uint64_t major = (uint64_t)no / 2 + 1;
+    int64_t hdr = 1 + 3 + 8 + 1 + digits(major) + 1 + 1 + 1 + digits(major) + 8 + digits((uint64_t)L) + 1;
+    return 2 * hdr + 2 * (int64_t)(L + 1);
+}
+
+int64_t write_rec(char *p, uint64_t seed, int64_t no, int L) {
+    uint64_t s = seed * 0xD1B54A32D192ED03ull ^ ((uint64_t)no * 0x9E3779B97F4A7C15ull) ^ 0x5851F42D4C957F2Dull;
+    splitmix(s);
+    char *p0 = p;
+    uint64_t major = (uint64_t)no / 2 + 1, minor = (uint64_t)no % 2 + 1;
+    for (int line = 0; line < 2; line++) {
+        // header ('@') then, after the sequence, the '+' line with a fresh id (Generator.cs:11-14)
+        if (line == 1) {
+            for (int i = 0; i < L; i += 32) {
+                uint64_t r = splitmix(s);
+                int m = L - i < 32 ? L - i : 32;
+                for (int b = 0; b < m; b++) { p[i + b] = "ATCG"[r & 3]; r >>= 2; }
+            }
+            p += L;
+            *p++ = '\n';
+        }
+        *p++ = line == 0 ? '@' : '+';
+        memcpy(p, "SRR", 3); p += 3;
+        p += put_u(p, 10000000ull + splitmix(s) % 10000000ull);
+        *p++ = '.'; p += put_u(p, major); *p++ = '.'; p += put_u(p, minor);
+        *p++ = ' '; p += put_u(p, major);
+        memcpy(p, " length=", 8); p += 8;
+        p += put_u(p, (uint64_t)L);
+        *p++ = '\n';
+    }
+    for (int i = 0; i < L; i += 4) {
+        uint64_t r = splitmix(s);
+        int m = L - i < 4 ? L - i : 4;
+        for (int b = 0; b < m; b++) {
+            uint32_t u = (uint32_t)(r & 0xFFFF); r >>= 16;
+            p[i + b] = u < 58982u ? '?' : (u < 62259u ? '*' : '!');   // .90 / .05 / .05
+        }
+    }
+    p += L;
+    *p++ = '\n';
+    return p - p0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// exact byte size of records [no0, no0+n)
+int64_t ppg_synth_fastq_size(int64_t no0, int64_t n, int read_len) {
+    int64_t t = 0;
+    for (int64_t no = no0; no < no0 + n; no++) t += rec_size(no, read_len);
+    return t;
+}
+
+// Writes records [no0, no0+n) into out (cap bytes).  Returns bytes written or -1.
+int64_t ppg_synth_fastq(uint64_t seed, int64_t no0, int64_t n, int read_len, uint8_t *out, int64_t cap,
+                        int threads) {
+    if (threads < 1) threads = 1;
+    int64_t per = (n + threads - 1) / threads;
+    std::vector<int64_t> off(threads + 1, 0);
+    for (int t = 0; t < threads; t++) {
+        int64_t a = no0 + std::min(n, t * per), b = no0 + std::min(n, (t + 1) * per);
+        off[t + 1] = off[t] + ppg_synth_fastq_size(a, b - a, read_len);
+    }
+    if (off[threads] > cap) return -1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        th.emplace_back([=, &off] {
+            int64_t a = no0 + std::min(n, t * per), b = no0 + std::min(n, (t + 1) * per);
+            char *p = (char *)out + off[t];
+            for (int64_t no = a; no < b; no++) p += write_rec(p, seed, no, read_len);
+        });
+    }
+    for (auto &x : th) x.join();
+    return off[threads];
+}
+
+// Raw-deflates text[lo,hi) primed with dict (dlen<=32768); `last` -> Z_FINISH, else Z_SYNC_FLUSH.
+static int64_t deflate_piece(const uint8_t *text, int64_t lo, int64_t hi, const uint8_t *dict, int dlen,
+                             int level, int last, std::vector<uint8_t> &out) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -1;
+    if (dlen > 0) deflateSetDictionary(&zs, dict, (uInt)dlen);
+    out.resize((size_t)deflateBound(&zs, (uLong)(hi - lo)) + 64);
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)out.size();
+    int64_t pos = lo;
+    const int64_t STEP = 1 << 30;
+    int ret;
+    do {
+        int64_t n = std::min(STEP, hi - pos);
+        zs.next_in = (Bytef *)(text + pos);
+        zs.avail_in = (uInt)n;
+        pos += n;
+        int flush = pos < hi ? Z_NO_FLUSH : (last ? Z_FINISH : Z_SYNC_FLUSH);
+        ret = deflate(&zs, flush);
+        if (ret == Z_STREAM_ERROR) { deflateEnd(&zs); return -1; }
+    } while (pos < hi);
+    int64_t got = (int64_t)zs.total_out;
+    deflateEnd(&zs);
+    out.resize((size_t)got);
+    return got;
+}
+
+static void put_le32(uint8_t *p, uint32_t v) { for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i)); }
+
+// Single-member gzip of text.  piece<=0 -> one serial deflate (byte-identical to zlib's
+// own gzip wrapper output at that level); piece>0 -> pigz-style parallel pieces.
+// Returns the .gz length, or -1 if cap is too small.
+int64_t ppg_synth_gzip(const uint8_t *text, int64_t len, int level, int64_t piece, int threads, uint8_t *out,
+                       int64_t cap) {
+    if (piece <= 0) piece = len > 0 ? len : 1;
+    int64_t np = (len + piece - 1) / piece;
+    if (np == 0) np = 1;
+    std::vector<std::vector<uint8_t>> parts((size_t)np);
+    std::vector<uint32_t> crcs((size_t)np);
+    std::atomic<int64_t> next{0};
+    std::atomic<int> bad{0};
+    if (threads < 1) threads = 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        th.emplace_back([&] {
+            for (;;) {
+                int64_t i = next.fetch_add(1);
+                if (i >= np) break;
+                int64_t lo = i * piece, hi = std::min(len, lo + piece);
+                int64_t dl = std::min<int64_t>(lo, 32768);
+                if (deflate_piece(text, lo, hi, text + lo - dl, (int)dl, level, i == np - 1, parts[i]) < 0) bad = 1;
+                crcs[i] = (uint32_t)crc32(0L, text + lo, (uInt)(hi - lo));
+            }
+        });
+    }
+    for (auto &x : th) x.join();
+    if (bad) return -1;
+    int64_t tot = 10 + 8;
+    for (auto &p : parts) tot += (int64_t)p.size();
+    if (tot > cap) return -1;
+    static const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 3};
+    memcpy(out, hdr, 10);
+    uint8_t *w = out + 10;
+    uLong crc = 0;
+    for (int64_t i = 0; i < np; i++) {
+        memcpy(w, parts[i].data(), parts[i].size());
+        w += parts[i].size();
+        int64_t lo = i * piece, hi = std::min(len, lo + piece);
+        crc = crc32_combine(crc, crcs[i], (z_off_t)(hi - lo));
+    }
+    put_le32(w, (uint32_t)crc);
+    put_le32(w + 4, (uint32_t)len);
+    return tot;
+}
+
+// ---- tiled member -------------------------------------------------------------------------
+// Segment deflate: text deflated as pigz pieces, first piece without dictionary, every piece
+// closed by Z_SYNC_FLUSH (so the segment ends byte-aligned and references nothing before it).
+// seg_out receives the raw deflate bytes; returns their length.
+int64_t ppg_synth_segment(const uint8_t *text, int64_t len, int level, int64_t piece, int threads,
+                          uint8_t *seg_out, int64_t cap, uint32_t *crc_out) {
+    if (piece <= 0) piece = len;
+    int64_t np = (len + piece - 1) / piece;
+    std::vector<std::vector<uint8_t>> parts((size_t)np);
+    std::atomic<int64_t> next{0};
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, threads); t++) {
+        th.emplace_back([&] {
+            for (;;) {
+                int64_t i = next.fetch_add(1);
+                if (i >= np) break;
+                int64_t lo = i * piece, hi = std::min(len, lo + piece);
+                int64_t dl = std::min<int64_t>(lo, 32768);
+                if (deflate_piece(text, lo, hi, text + lo - dl, (int)dl, level, 0, parts[i]) < 0) bad = 1;
+            }
+        });
+    }
+    for (auto &x : th) x.join();
+    if (bad) return -1;
+    int64_t tot = 0;
+    for (auto &p : parts) tot += (int64_t)p.size();
+    if (tot > cap) return -1;
+    uint8_t *w = seg_out;
+    for (auto &p : parts) { memcpy(w, p.data(), p.size()); w += p.size(); }
+    *crc_out = (uint32_t)crc32(0L, text, (uInt)0);
+    {
+        uLong c = 0;
+        int64_t pos = 0;
+        while (pos < len) {
+            int64_t n = std::min<int64_t>(len - pos, 1 << 30);
+            c = crc32(c, text + pos, (uInt)n);
+            pos += n;
+        }
+        *crc_out = (uint32_t)c;
+    }
+    return tot;
+}
+
+// gzip header (10 B) and the tail that closes a tiled member: an empty final fixed block
+// (bits 1,01,0000000 -> 0x03 0x00) + CRC-32 + ISIZE of S^T.
+void ppg_synth_tiled_frame(uint32_t seg_crc, int64_t seg_len, int64_t repeats, uint8_t *hdr10, uint8_t *tail10) {
+    static const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 3};
+    memcpy(hdr10, hdr, 10);
+    uLong crc = 0;
+    for (int64_t r = 0; r < repeats; r++) crc = crc32_combine(crc, seg_crc, (z_off_t)seg_len);
+    tail10[0] = 0x03;
+    tail10[1] = 0x00;
+    put_le32(tail10 + 2, (uint32_t)crc);
+    put_le32(tail10 + 6, (uint32_t)((uint64_t)seg_len * (uint64_t)repeats));
+}
+
+// Deflate block ends of the segment (raw stream, no dictionary), found exactly as CreateIndex
+// sees them: inflate(Z_BLOCK) returns with data_type bit 128 (Core.cs:64,98).  Writes, per block
+// end, its bit position within the segment and its output position.  Returns the count.
+int64_t ppg_synth_segment_blocks(const uint8_t *seg, int64_t seg_len, int64_t text_len, int64_t *bit_end,
+                                 int64_t *out_end, int64_t cap) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return -1;
+    std::vector<uint8_t> win(1 << 20);
+    int64_t n = 0, totin = 0, totout = 0, pos = 0;
+    int ret = Z_OK;
+    zs.avail_out = 0;
+    (void)text_len;
+    for (;;) {
+        if (zs.avail_in == 0) {  // every byte of the segment is consumed, so trailing empty blocks count
+            int64_t k = std::min<int64_t>(seg_len - pos, 1 << 20);
+            if (k <= 0) break;
+            zs.next_in = (Bytef *)(seg + pos);
+            zs.avail_in = (uInt)k;
+            pos += k;
+        }
+        if (zs.avail_out == 0) { zs.next_out = win.data(); zs.avail_out = (uInt)win.size(); }
+        totin += zs.avail_in; totout += zs.avail_out;
+        ret = inflate(&zs, Z_BLOCK);
+        totin -= zs.avail_in; totout -= zs.avail_out;
+        if (ret != Z_OK && ret != Z_BUF_ERROR) { inflateEnd(&zs); return -1; }
+        if ((zs.data_type & 128) && !(zs.data_type & 64)) {
+            if (n < cap) { bit_end[n] = 8 * totin - (zs.data_type & 7); out_end[n] = totout; }
+            n++;
+        }
+    }
+    inflateEnd(&zs);
+    return n;
+}
+
+// CreateIndex points of the tiled file  hdr(10) + seg^T + tail  (Core.cs:14-131), from the
+// segment block list.  Point fields are written into caller arrays sized for `cap` points:
+// output/input/bits, window (32768 B each), and offsets (concatenated; off_len per point,
+// off_cap bytes total).  Returns the point count, -1 if a buffer is short, -2 on Q4 overflow.
+int64_t ppg_synth_tiled_points(const uint8_t *text, int64_t text_len, int64_t seg_gz_len, int64_t repeats,
+                               const int64_t *bit_end, const int64_t *out_end, int64_t nblocks, uint32_t chunksize,
+                               int64_t *p_output, int64_t *p_input, int32_t *p_bits, uint8_t *p_window,
+                               int32_t *p_off_len, uint8_t *p_off, int64_t off_cap, int64_t cap) {
+    // '@' prefix counts over one segment: at[x] = '@' count in text[0,x) sampled at block ends.
+    std::vector<int64_t> at_blk((size_t)nblocks);
+    std::vector<int64_t> last_at_blk((size_t)nblocks);  // position of last '@' before out_end (or -1)
+    {
+        int64_t cnt = 0, last = -1, x = 0;
+        for (int64_t b = 0; b < nblocks; b++) {
+            for (; x < out_end[b]; x++) if (text[x] == '@') { cnt++; last = x; }
+            at_blk[b] = cnt;
+            last_at_blk[b] = last;
+        }
+        for (; x < text_len; x++) if (text[x] == '@') { cnt++; last = x; }
+        // total per segment
+        at_blk.push_back(cnt);
+        last_at_blk.push_back(last);
+    }
+    const int64_t seg_at = at_blk[(size_t)nblocks];
+    const int64_t seg_last_at = last_at_blk[(size_t)nblocks];
+    int64_t np = 0, off_used = 0;
+    auto emit = [&](int64_t output, int64_t input, int bits, int64_t at_pos_abs) -> int {
+        if (np >= cap) return -1;
+        p_output[np] = output; p_input[np] = input; p_bits[np] = bits;
+        uint8_t *w = p_window + (size_t)np * 32768;
+        // last 32 KiB of S^T before `output`, zero-filled before the stream start (Index.cs:42-46)
+        for (int64_t i = 0; i < 32768; i++) {
+            int64_t q = output - 32768 + i;
+            w[i] = q < 0 ? 0 : text[q % text_len];
+        }
+        int32_t ol = 0;
+        if (at_pos_abs >= 0) {
+            if (output - at_pos_abs > 32768) return -2;
+            ol = (int32_t)(output - at_pos_abs);
+            if (off_used + ol > off_cap) return -1;
+            for (int32_t i = 0; i < ol; i++) p_off[off_used + i] = text[(at_pos_abs + i) % text_len];
+        }
+        p_off_len[np] = ol;
+        off_used += ol;
+        np++;
+        return 0;
+    };
+    // first point right after the gzip header (totout == 0, Core.cs:101-102): no offset bytes
+    if (emit(0, 10, 0, -1) < 0) return -1;
+    int64_t counter_base = 0;  // '@' count at the last point
+    const int64_t seg_bits = seg_gz_len * 8;
+    const int64_t thresh = (int64_t)(uint32_t)(chunksize - 8u);
+    for (int64_t r = 0; r < repeats; r++) {
+        for (int64_t b = 0; b < nblocks; b++) {
+            int64_t out_abs = r * text_len + out_end[b];
+            int64_t at_abs = r * seg_at + at_blk[b];
+            if (out_abs == 0) {  // a block end before any output also creates a point
+                int64_t bitpos = 80 + r * seg_bits + bit_end[b];
+                int64_t totin = (bitpos + 7) / 8;
+                int rc = emit(0, totin, (int)(totin * 8 - bitpos), -1);
+                if (rc < 0) return rc;
+                continue;
+            }
+            if (at_abs - counter_base > thresh) {
+                int64_t bitpos = 80 + r * seg_bits + bit_end[b];
+                int64_t totin = (bitpos + 7) / 8;
+                int64_t last_abs;
+                if (last_at_blk[b] >= 0) last_abs = r * text_len + last_at_blk[b];
+                else if (r > 0 && seg_last_at >= 0) last_abs = (r - 1) * text_len + seg_last_at;
+                else last_abs = -1;
+                if (last_abs < 0) return -2;  // offset would hold the whole prefix (not our data)
+                int rc = emit(out_abs, totin, (int)(totin * 8 - bitpos), last_abs);
+                if (rc < 0) return rc;
+                counter_base = at_abs;
+            }
+        }
+    }
+    // final point at stream end (Core.cs:123): bits 0, input = file length, output = |S|*T
+    int64_t flen = 10 + repeats * seg_gz_len + 10;
+    if (emit(repeats * text_len, flen, 0, -1) < 0) return -1;
+    return np;
+}
+
+}  // extern "C"

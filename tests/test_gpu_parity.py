@@ -1,0 +1,145 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures and the oracle.
+
+Bit-exact decompressed bytes and identical per-chunk Parsing.Parse record tables are required
+(integer/byte work: no tolerance)."""
+import hashlib
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import parallelparsing_amd as pp
+from conftest import CASES, CORRUPT, GOLDEN, load_case
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(b):
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def comp_range(gz, index, first, n):
+    _, i0, _, _ = index.point_fields(first)
+    _, i1, _, _ = index.point_fields(first + n)
+    return np.frombuffer(gz[i0 - 1:i1], np.uint8)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_shard_matches_golden(name, device):
+    meta, gz = load_case(name)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    assert ix.Count == meta["points"]
+    n = ix.Count - 1
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+    r = sh.results()
+    assert (r["status"] == 0).all()
+    for k, c in enumerate(meta["chunks"]):
+        b = sh.chunk_bytes(k)
+        assert len(b) == c["out_len"], (name, k)
+        assert sha(b) == c["sha256"], (name, k)
+        rec = sh.chunk_records(k)
+        assert len(rec) == c["records"], (name, k)
+        assert sha(np.ascontiguousarray(rec, "<u4").tobytes()) == c["rec_sha256"], (name, k)
+        # R-E5: the chunk ends right before its block's end-of-block code (flag bits 1|2|4)
+        if k < n - 1:
+            assert r["flags"][k] & 7 == 0, (name, k, r["flags"][k])
+    assert sh.total_records == meta["total_records"]
+
+
+@pytest.mark.parametrize("name", ["l6_c20", "memlevel1_c10", "stored_c50", "huffonly_c20"])
+def test_extract_single_chunk(name, device):
+    """README "Decompress": one checkpoint from the LazyFileReader slice (Core.cs:133-192)."""
+    meta, gz = load_case(name)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    for k in range(ix.Count - 1):
+        sl = comp_range(gz, ix, k, 1)
+        got, buf, rec = pp.Core.ExtractDeflateIndex(sl, ix, k, device=device, with_records=True)
+        assert got == meta["chunks"][k]["out_len"]
+        assert sha(buf[:got]) == meta["chunks"][k]["sha256"]
+        assert len(rec) == meta["chunks"][k]["records"]
+
+
+@pytest.mark.parametrize("name", CORRUPT)
+def test_corrupt_streams(name, device):
+    """Corrupted compressed bytes: the same DATA_ERROR as zlib, or the same garbage bytes."""
+    meta, gz = load_case(name)
+    with open(os.path.join(GOLDEN, "corrupt_clean.gz"), "rb") as f:
+        ix = pp.Core.BuildDeflateIndex(f.read(), meta["chunksize"])
+    k = meta["chunk"]
+    sh = pp.Shard(ix, comp_range(gz, ix, k, 1), k, 1, device=device)
+    if meta["oracle_status"] != 0:
+        with pytest.raises(pp.PpgError) as e:
+            sh.run()
+        assert e.value.code == meta["oracle_status"]
+    else:
+        sh.run()
+        b = sh.chunk_bytes(0)
+        assert len(b) == meta["out_len"] and sha(b) == meta["out_sha256"]
+
+
+def test_batched_output_matches_single_batch(device):
+    """out_capacity forces several batches through one reused output buffer."""
+    meta, gz = load_case("memlevel1_c10")
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    n = ix.Count - 1
+    one = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run().results()
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device, out_capacity=8192)
+    assert sh.batches > 4
+    many = sh.run().results()
+    for key in ("records", "produced", "status"):
+        assert (one[key] == many[key]).all(), key
+    assert sh.total_records == meta["total_records"]
+
+
+def test_batched_fastq_fields_match_oracle(tmp_path, device):
+    """BatchedFASTQ (DecompressAll) record fields == the oracle's Parsing.Parse, chunk order."""
+    meta, gz = load_case("l6_c20")
+    p = tmp_path / "x.fastq.gz"
+    p.write_bytes(gz)
+    ix = pp.Core.BuildDeflateIndex(str(p), meta["chunksize"])
+    pp.IndexIO.Serialize(ix, str(tmp_path / "x.gzi"))
+    bf = pp.BatchedFASTQ(str(tmp_path / "x.gzi"), str(p), False, device=device)
+    assert bf.Count() == meta["total_records"]
+    recs = list(bf)
+    oi = O.build_index(gz, meta["chunksize"])
+    exp = []
+    for k in range(oi.count - 1):
+        off = oi.point(k)[4]
+        ch = O.extract(gz, oi, k)
+        raw = off + ch
+        exp += pp.records_from_descriptors(raw, O.parse(off, ch))
+    assert len(recs) == len(exp)
+    for a, b in zip(recs, exp):
+        assert (a.identifier, a.sequence, a.other, a.quality) == (b.identifier, b.sequence, b.other, b.quality)
+
+
+def test_larger_file_vs_oracle_and_trailer(device):
+    """200k records (~75 MB text), chunk 10000: every chunk vs the oracle, and the CRC-32 of
+    the GPU output against the gzip trailer (a size-independent whole-stream check)."""
+    import ctypes as C
+    S = pp.synth()
+    nrec = 200_000
+    sz = S.ppg_synth_fastq_size(0, nrec, 150)
+    txt = np.zeros(sz, np.uint8)
+    S.ppg_synth_fastq(99, 0, nrec, 150, C.c_void_p(txt.ctypes.data), sz, 8)
+    gzb = np.zeros(sz, np.uint8)
+    L = S.ppg_synth_gzip(C.c_void_p(txt.ctypes.data), sz, 6, 4 << 20, 8, C.c_void_p(gzb.ctypes.data), gzb.size)
+    gz = gzb[:L].tobytes()
+    ix = pp.Core.BuildDeflateIndex(gz, 10000)
+    n = ix.Count - 1
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+    oi = O.build_index(gz, 10000)
+    crc = 0
+    tot = 0
+    for k in range(n):
+        b = sh.chunk_bytes(k)
+        exp = O.extract(gz, oi, k)
+        assert b.tobytes() == exp, k
+        rec = sh.chunk_records(k)
+        assert np.array_equal(rec, O.parse(oi.point(k)[4], exp)), k
+        crc = zlib.crc32(b.tobytes(), crc)
+        tot += len(rec)
+    assert crc == int.from_bytes(gz[-8:-4], "little")
+    assert tot == sh.total_records == nrec   # zlib -6 never places a Point at a record start here
