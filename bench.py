@@ -1,0 +1,205 @@
+"""bench.py — DecompressAll (BatchedFASTQ.Count()) on MI355X: FASTQ records/s + decompressed MB/s.
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on): a ~50 GB synthetic
+single-member .fastq.gz of 150 bp Generator-shape reads (~530 M records, ~205 GB decompressed),
+chunk = 10,000 records.  The member is "tiled" (parallelparsing_amd/tiled.py): one ~1 GB-text
+segment deflated once (zlib level 6, pigz-style pieces) and repeated inside one member, so it can
+be built on the box in seconds; its CreateIndex points are derived exactly (tests/test_tiled.py).
+The compressed bytes and the index (windows + offsets) are resident in HBM before timing; the
+timed step is one DecompressAll pass over every chunk of this rank's shard: HIP inflate +
+FASTQ record scan + descriptor emission, plus the all-gather of per-chunk record counts when
+N > 1.  Decompressed output streams through a reused device buffer (out_capacity), as a
+consumer enumerating records would.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 50gb|1m]
+  (N > 1: launched by torch.distributed.run, one process per GPU, backend nccl = RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+REFERENCE_REC_S = 1.217e6  # Plots/csv_original/parallel_10k_false.csv:8 (Arm64, published; not this metric)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_input(args):
+    from parallelparsing_amd.tiled import TiledFile
+    t = time.time()
+    if args.workload == "50gb":
+        # weak scaling: the member holds `repeats` segments per rank (~50 GB of gzip per GPU)
+        tf = TiledFile(args.seg_records, args.repeats * args.world, args.chunk, threads=args.host_threads)
+    else:  # 1m: configs[1], one non-repeated 1 M-read member
+        tf = TiledFile(1_000_000, 1, args.chunk, threads=args.host_threads)
+    log(f"[bench] input: {tf.records * tf.repeats:,} records, {tf.text_len * tf.repeats / 1e9:.1f} GB text, "
+        f"{tf.file_len / 1e9:.2f} GB gz, {tf.npoints - 1} chunks, built in {time.time() - t:.1f}s")
+    return tf
+
+
+def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
+    """The oracle's threaded DecompressAll (C restatement of BatchedFASTQ over zlib 1.2.11) on a
+    bounded prefix of the same file, timed on this host (rank 0, N = 1 only)."""
+    from oracle import oracle as O
+    sample = min(nchunks, int(os.environ.get("PPG_CPU_SAMPLE_CHUNKS", "2048")))
+    hi = int(ix_in[sample])
+    gz = tf.file_bytes(0, hi)
+    win, offs = tf.windows(0, sample + 1)
+    oi = O.index_from_points(tf.p_output[: sample + 1], tf.p_input[: sample + 1], tf.p_bits[: sample + 1],
+                             win, tf.p_offlen[: sample + 1], offs)
+    O.decompress_all(gz, oi, threads=threads, first=0, last=min(sample, 16))   # warm
+    t = time.perf_counter()
+    recs, _ = O.decompress_all(gz, oi, threads=threads, first=0, last=sample)
+    dt = time.perf_counter() - t
+    out_bytes = int(ix_out[sample] - ix_out[0])
+    return {"value": recs / dt, "unit": "records/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample} of {nchunks} chunks ({recs:,} records, {out_bytes / 1e9:.2f} GB out) "
+                      f"of the same file, {threads} threads, {dt:.2f} s",
+            "decompressed_MBps": out_bytes / dt / 1e6}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="50gb", choices=["50gb", "1m"])
+    ap.add_argument("--chunk", type=int, default=10000)
+    ap.add_argument("--seg-records", type=int, default=2_621_440)   # ~1 GB of text per segment
+    ap.add_argument("--repeats", type=int, default=203)             # per GPU: ~50 GB gz, ~532 M records
+    ap.add_argument("--out-capacity-gib", type=float, default=64.0)
+    ap.add_argument("--host-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    args.world = world
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import parallelparsing_amd as pp
+    from parallelparsing_amd.dist import partition_chunks, gather_counts
+
+    tf = build_input(args)
+    ix_out, ix_in = tf.p_output, tf.p_input
+    nchunks = tf.npoints - 1
+    ranges = partition_chunks(ix_in, world)
+    a, b = ranges[rank]
+    lo, hi = int(ix_in[a]) - 1, int(ix_in[b])   # file bytes [Input_a - 1, Input_b - 1]
+    comp_len = hi - lo
+    t = time.time()
+    comp = torch.empty(comp_len + 256, dtype=torch.uint8, device=dev)
+    comp[comp_len:].zero_()
+    tf.fill_device(comp, lo, hi)
+    torch.cuda.synchronize()
+    index = tf.index(a, b + 1)   # this rank's points only: its chunks are index chunks 0..b-a-1
+    ctx = pp.Device(local)
+    out_cap = int(args.out_capacity_gib * (1 << 30))
+    shard = pp.Shard(index, comp.data_ptr(), first=0, n=b - a, device=ctx, comp_on_device=True, comp_len=comp_len,
+                     out_capacity=out_cap)
+    log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
+        f"{shard.batches} output batch(es), setup {time.time() - t:.1f}s")
+    counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
+
+    def step():
+        shard.run()
+        if world > 1:
+            shard.counts_to_device(counts_dev.data_ptr())
+            return gather_counts(counts_dev[: b - a], ranges, device=dev)
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    infl_ms = parse_ms = 0.0
+    for _ in range(args.steps):
+        g = step()
+        tm = shard.timing()
+        infl_ms += tm["inflate_ms"]
+        parse_ms += tm["parse_ms"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    # correctness of the run (size-independent checks; bit parity is tests/test_gpu_parity.py)
+    r = shard.results()
+    assert (r["status"] == 0).all(), "chunk errors"
+    assert (r["produced"] == (ix_out[a + 1:b + 1] - ix_out[a:b])).all(), "produced != to.Output - from.Output"
+    local_records = int(r["records"].sum())
+    if world > 1:
+        counts, bases = g
+        total_records = int(counts.sum())
+    else:
+        total_records = local_records
+    expect = tf.records * tf.repeats
+    assert total_records == expect, (total_records, expect)
+
+    text_bytes = int(ix_out[-1] - ix_out[0])
+    comp_total = int(ix_in[-1] - ix_in[0])
+    rec_s = total_records * args.steps / elapsed
+    # roofline of the dominant kernel (inflate): algorithmic bytes per launch / its mean duration
+    alg_local = int((ix_in[a + 1:b + 1] - ix_in[a:b] + 1).sum() + (ix_out[a + 1:b + 1] - ix_out[a:b]).sum())
+    launches = shard.batches * args.steps
+    mean_launch_s = infl_ms / 1e3 / launches
+    achieved = alg_local / shard.batches / mean_launch_s / 1e9
+    line = {
+        "metric": "FASTQ records/sec + decompressed MB/s, 50 GB .fastq.gz, 1/2/4/8 MI355X",
+        "value": rec_s,
+        "unit": "records/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)",
+        "config": {"workload": ("configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000" if args.workload == "50gb"
+                                else "configs[1]: 1 M-read .fastq.gz, chunk=10000"),
+                   "records": total_records, "gz_bytes": tf.file_len, "decompressed_bytes": text_bytes,
+                   "chunks": nchunks, "parallelism": f"chunk-sharded x{world}"},
+        "decompressed_MBps": text_bytes * args.steps / elapsed / 1e6,
+        "kernel_ms_per_step": {"inflate": infl_ms / args.steps, "parse": parse_ms / args.steps},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "ppg_inflate_kernel", "alg_bytes_per_launch": alg_local / shard.batches,
+                     "mean_launch_ms": mean_launch_s * 1e3},
+        "reference_published_rec_s": REFERENCE_REC_S,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(tf, ix_out, ix_in, nchunks, threads)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

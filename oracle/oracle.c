@@ -327,6 +327,26 @@ bad:
     return ORC_IO_ERROR;
 }
 
+/* Index from point arrays (windows count*32768 bytes, offsets concatenated) — lets the CPU
+ * baseline run on an index produced elsewhere (the bench's tiled file). */
+int orc_index_from_points(int count, const int64_t *output, const int64_t *input, const int32_t *bits,
+                          const uint8_t *windows, const int32_t *offset_len, const uint8_t *offsets, orc_index **out) {
+    orc_index *ix = idx_new();
+    int64_t o = 0;
+    for (int i = 0; i < count; i++) {
+        orc_point *p = idx_push(ix);
+        p->output = output[i]; p->input = input[i]; p->bits = bits[i];
+        p->window = (uint8_t *)malloc(WINSIZE);
+        memcpy(p->window, windows + (size_t)i * WINSIZE, WINSIZE);
+        p->offset_len = offset_len[i];
+        p->offset = (uint8_t *)malloc(offset_len[i] > 0 ? (size_t)offset_len[i] : 1);
+        if (offset_len[i] > 0) memcpy(p->offset, offsets + o, (size_t)offset_len[i]);
+        o += offset_len[i];
+    }
+    *out = ix;
+    return 0;
+}
+
 /* ---- accessors for ctypes ---- */
 int orc_index_count(const orc_index *ix) { return ix->count; }
 int32_t orc_index_chunk_max_bytes(const orc_index *ix) { return ix->chunk_max_bytes; }

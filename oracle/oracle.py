@@ -46,6 +46,8 @@ def _load():
     L.orc_serialize.argtypes = [vp, C.c_char_p]
     L.orc_deserialize.restype = C.c_int
     L.orc_deserialize.argtypes = [C.c_char_p, C.POINTER(vp)]
+    L.orc_index_from_points.restype = C.c_int
+    L.orc_index_from_points.argtypes = [C.c_int, vp, vp, vp, vp, vp, vp, C.POINTER(vp)]
     L.orc_decompress_all.restype = i64
     L.orc_decompress_all.argtypes = [vp, vp, i64, C.c_int, C.c_int, C.c_int, C.c_int, vp]
     return L
@@ -99,6 +101,16 @@ def build_index(gz, chunksize):
     rc = L.orc_build_index(C.c_void_p(a.ctypes.data), a.size, chunksize & 0xFFFFFFFF, C.byref(h))
     if rc:
         raise OracleError(rc)
+    return OracleIndex(h.value)
+
+
+def index_from_points(output, inp, bits, windows, offset_len, offsets):
+    a = [np.ascontiguousarray(x, t) for x, t in ((output, np.int64), (inp, np.int64), (bits, np.int32),
+                                                  (windows, np.uint8), (offset_len, np.int32))]
+    offs = np.ascontiguousarray(offsets if len(offsets) else np.zeros(1), np.uint8)
+    h = C.c_void_p()
+    L.orc_index_from_points(len(a[0]), *[C.c_void_p(x.ctypes.data) for x in a], C.c_void_p(offs.ctypes.data),
+                            C.byref(h))
     return OracleIndex(h.value)
 
 

@@ -111,6 +111,8 @@ def synth():
         s.ppg_synth_segment_blocks.restype = i64
         s.ppg_synth_segment_blocks.argtypes = [vp, i64, i64, vp, vp, i64]
         s.ppg_synth_tiled_points.restype = i64
-        s.ppg_synth_tiled_points.argtypes = [vp, i64, i64, i64, vp, vp, i64, u32, vp, vp, vp, vp, vp, vp, i64, i64]
+        s.ppg_synth_tiled_points.argtypes = [vp, i64, i64, i64, vp, vp, i64, u32, vp, vp, vp, vp, vp, i64]
+        s.ppg_synth_tiled_fill.restype = None
+        s.ppg_synth_tiled_fill.argtypes = [vp, i64, vp, vp, vp, i64, i64, vp, vp]
         _synth = s
     return _synth

@@ -22,10 +22,11 @@
 #include "../../include/ppgpu.h"
 #include "ppg_device.h"
 
-// launchers (ppg_kernels.hip)
-size_t ppg_inflate_lds_bytes();
-hipError_t ppg_launch_inflate(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
-                              const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, int njobs);
+// launchers (ppg_inflate.hip, ppg_parse.hip)
+size_t ppg_inflate_lds_bytes(int ring_bits);
+hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, const uint32_t *comp, uint64_t nwords,
+                              const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
+                              int njobs);
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n);
@@ -332,6 +333,7 @@ const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    int ring_bits = 14;   // inflate history ring: 2^13..2^15 bytes of LDS per wavefront
 };
 
 namespace {
@@ -379,6 +381,7 @@ int ppg_open(int device, ppg_ctx **out) {
     auto ctx = std::make_unique<ppg_ctx>();
     ctx->device = device;
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(13, atoi(rb)));
     *out = ctx.release();
     return PPG_OK;
 }
@@ -520,8 +523,9 @@ int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n
     // output + a 64-byte tail: the parse kernels read whole 16-B words
     HIPCHK(sh->out.alloc((size_t)sh->out_cap + 64));
     HIPCHK(hipMemsetAsync(sh->out.p + sh->out_cap, 0, 64, s));
-    // descriptor space: FASTQ records are >> 64 B; the run grows it if a batch needs more
-    HIPCHK(sh->recs.alloc((size_t)(4 * (sh->out_cap / 64 + 1024))));
+    // descriptor space (16 B per record) sized for >= 256-B records; a batch that needs more
+    // grows it before its emit pass (ppg_shard_run)
+    HIPCHK(sh->recs.alloc((size_t)(4 * (sh->out_cap / 256 + 1024))));
     for (auto &e : sh->ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipStreamSynchronize(s));
     *out = sh.release();
@@ -539,8 +543,8 @@ int ppg_shard_run(ppg_shard *sh) {
     for (auto [b0, b1] : sh->batches) {
         const int nb = b1 - b0;
         HIPCHK(hipEventRecord(sh->ev[0], s));
-        HIPCHK(ppg_launch_inflate(s, (const uint32_t *)sh->comp, sh->nwords, sh->jobs.p + b0, sh->dicts.p, sh->out.p,
-                                  sh->res.p + b0, nb));
+        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, (const uint32_t *)sh->comp, sh->nwords, sh->jobs.p + b0,
+                                  sh->dicts.p, sh->out.p, sh->res.p + b0, nb));
         HIPCHK(hipEventRecord(sh->ev[1], s));
         HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
                                       sh->info.p + b0, sh->base.p + b0, sh->total.p, nb));

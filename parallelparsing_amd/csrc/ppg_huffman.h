@@ -1,0 +1,161 @@
+// ppg_huffman.h — device-side DEFLATE (RFC 1951) Huffman machinery shared by the inflate kernel:
+// canonical table build by 64 lanes, the zlib 1.2.11 validity rules, and the bit-serial slow path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LB 10            // litlen root table bits
+#define DB 8             // distance root table bits
+#define CB 7             // code-length-code table bits (complete: max code length is 7)
+#define UNIT 4096        // flush unit (bytes, global-address aligned)
+
+// table entry: [3:0] code length (0 = slow path) [5:4] kind [15:8] literal / extra bits [31:16] base
+#define K_LIT 0u
+#define K_BASE 1u
+#define K_EOB 2u
+#define K_BAD 3u
+
+
+__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385,
+                                     513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+enum { TAB_LIT = 0, TAB_DST = 1, TAB_CL = 2 };
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
+}
+
+__device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int kind) {
+    if (kind == TAB_CL) return len | (sym << 8);
+    if (kind == TAB_LIT) {
+        if (sym < 256) return len | (K_LIT << 4) | (sym << 8);
+        if (sym == 256) return len | (K_EOB << 4);
+        if (sym < 286) return len | (K_BASE << 4) | ((uint32_t)c_lext[sym - 257] << 8) | ((uint32_t)c_lbase[sym - 257] << 16);
+        return len | (K_BAD << 4);
+    }
+    if (sym < 30) return len | (K_BASE << 4) | ((uint32_t)c_dext[sym] << 8) | ((uint32_t)c_dbase[sym] << 16);
+    return len | (K_BAD << 4);
+}
+
+// Builds a canonical-Huffman root table of 2^TB entries from n code lengths (all 64 lanes).
+// Codes longer than TB (and unused patterns of an incomplete code) get entry 0 -> slow path,
+// which decodes bit-by-bit from count[]/sorted[].  Validity follows zlib 1.2.11 inflate_table:
+// over-subscribed -> error; incomplete -> error unless exactly one code of length 1 (not for
+// the code-length code); no codes at all -> accepted (decoding then fails).  Returns 0 / -1.
+template <int TB>
+__device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t *count_lds, uint16_t *sorted,
+                           int kind, int lane) {
+    uint32_t cnt[16];
+#pragma unroll
+    for (int l = 0; l < 16; l++) cnt[l] = 0;
+    for (int g = 0; g < n; g += 64) {
+        int s = g + lane;
+        uint32_t L = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (int l = 1; l < 16; l++) cnt[l] += (uint32_t)__popcll(__ballot(L == (uint32_t)l));
+    }
+    int left = 1, maxl = 0;
+#pragma unroll
+    for (int l = 1; l < 16; l++) {
+        left = left * 2 - (int)cnt[l];
+        if (cnt[l]) maxl = l;
+    }
+    if (maxl != 0) {
+        if (left < 0) return -1;
+        if (left > 0 && (kind == TAB_CL || maxl != 1)) return -1;
+    } else if (kind == TAB_CL) {
+        return -1;  // zlib accepts the empty set, then fails with "missing end-of-block"
+    }
+    uint32_t offs[16], seen[16];
+    offs[0] = 0;
+    offs[1] = 0;
+#pragma unroll
+    for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
+#pragma unroll
+    for (int l = 0; l < 16; l++) seen[l] = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int g = 0; g < n; g += 64) {
+        int s = g + lane;
+        uint32_t L = s < n ? lens[s] : 0u;
+        uint32_t mypos = 0;
+#pragma unroll
+        for (int l = 1; l < 16; l++) {
+            uint64_t m = __ballot(L == (uint32_t)l);
+            if (L == (uint32_t)l) mypos = offs[l] + seen[l] + (uint32_t)__popcll(m & lt);
+            seen[l] += (uint32_t)__popcll(m);
+        }
+        if (L) sorted[mypos] = (uint16_t)s;
+    }
+    if (count_lds) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int l = 0; l < 16; l++) c = (lane == l) ? cnt[l] : c;
+        if (lane < 16) count_lds[lane] = (uint16_t)c;
+    }
+    __syncthreads();
+    for (int e0 = 0; e0 < (1 << TB); e0 += 64) {   // uniform trip count (see ppg_inflate_kernel)
+        const int e = e0 + lane;
+        uint32_t code = 0, first = 0, index = 0, entry = 0;
+#pragma unroll
+        for (int l = 1; l <= TB; l++) {
+            code |= ((uint32_t)e >> (l - 1)) & 1u;
+            uint32_t c = cnt[l];
+            if (entry == 0 && code - first < c) entry = make_entry(sorted[index + code - first], (uint32_t)l, kind);
+            index += c;
+            first = (first + c) << 1;
+            code <<= 1;
+        }
+        table[e] = entry;
+    }
+    __syncthreads();
+    return 0;
+}
+
+// Consume n (<= 32) bits from a reader's bit buffer (fields bb / bn).
+template <class R>
+__device__ __forceinline__ uint32_t br_take(R &b, uint32_t n) {
+    uint32_t v = (uint32_t)(b.bb & ((1ull << n) - 1ull));
+    b.bb >>= n;
+    b.bn -= n;
+    return v;
+}
+
+// Canonical bit-by-bit decode (codes longer than the root table, or invalid patterns).
+// Returns symbol, or -1 for an invalid code.  Needs bn >= 15.
+template <class R>
+__device__ int slow_decode(R &b, const uint16_t *count, const uint16_t *sorted) {
+    uint32_t code = 0, first = 0, index = 0;
+    for (uint32_t l = 1; l < 16; l++) {
+        code |= (uint32_t)(b.bb >> (l - 1)) & 1u;
+        uint32_t c = uni(count[l]);
+        if (code - first < c) {
+            uint32_t sym = uni(sorted[index + code - first]);
+            b.bb >>= l;
+            b.bn -= l;
+            return (int)sym;
+        }
+        index += c;
+        first = (first + c) << 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+// Slow path as a table entry (length field 0: the code is already consumed); K_BAD if invalid.
+template <class R>
+__device__ __forceinline__ uint32_t slow_entry(R &b, const uint16_t *count, const uint16_t *sorted, int kind) {
+    const int sym = slow_decode(b, count, sorted);
+    if (sym < 0) return K_BAD << 4;
+    return uni(make_entry((uint32_t)sym, 0, kind));
+}
+
+// status codes (ZResult, Interop/Conventions.cs:9-20)
+#define ST_OK 0
+#define ST_DATA_ERROR (-3)
+

@@ -294,86 +294,85 @@ int64_t ppg_synth_segment_blocks(const uint8_t *seg, int64_t seg_len, int64_t te
 }
 
 // CreateIndex points of the tiled file  hdr(10) + seg^T + tail  (Core.cs:14-131), from the
-// segment block list.  Point fields are written into caller arrays sized for `cap` points:
-// output/input/bits, window (32768 B each), and offsets (concatenated; off_len per point,
-// off_cap bytes total).  Returns the point count, -1 if a buffer is short, -2 on Q4 overflow.
+// segment block list: per point output / input / bits, the offset length and the absolute
+// position of the '@' that starts the offset (-1: no offset).  Windows and offset bytes are
+// filled separately for any point range (ppg_synth_tiled_fill), so each rank materialises only
+// its own.  Returns the point count, -1 if cap is short, -2 on Q4 overflow.
 int64_t ppg_synth_tiled_points(const uint8_t *text, int64_t text_len, int64_t seg_gz_len, int64_t repeats,
                                const int64_t *bit_end, const int64_t *out_end, int64_t nblocks, uint32_t chunksize,
-                               int64_t *p_output, int64_t *p_input, int32_t *p_bits, uint8_t *p_window,
-                               int32_t *p_off_len, uint8_t *p_off, int64_t off_cap, int64_t cap) {
-    // '@' prefix counts over one segment: at[x] = '@' count in text[0,x) sampled at block ends.
-    std::vector<int64_t> at_blk((size_t)nblocks);
-    std::vector<int64_t> last_at_blk((size_t)nblocks);  // position of last '@' before out_end (or -1)
-    {
-        int64_t cnt = 0, last = -1, x = 0;
-        for (int64_t b = 0; b < nblocks; b++) {
-            for (; x < out_end[b]; x++) if (text[x] == '@') { cnt++; last = x; }
-            at_blk[b] = cnt;
-            last_at_blk[b] = last;
-        }
-        for (; x < text_len; x++) if (text[x] == '@') { cnt++; last = x; }
-        // total per segment
-        at_blk.push_back(cnt);
-        last_at_blk.push_back(last);
+                               int64_t *p_output, int64_t *p_input, int32_t *p_bits, int32_t *p_off_len,
+                               int64_t *p_at, int64_t cap) {
+    // '@' census of one segment at every block end (count and position of the last '@')
+    std::vector<int64_t> at_blk((size_t)nblocks), last_at_blk((size_t)nblocks);
+    int64_t cnt = 0, last = -1, x = 0;
+    for (int64_t b = 0; b < nblocks; b++) {
+        for (; x < out_end[b]; x++) if (text[x] == '@') { cnt++; last = x; }
+        at_blk[(size_t)b] = cnt;
+        last_at_blk[(size_t)b] = last;
     }
-    const int64_t seg_at = at_blk[(size_t)nblocks];
-    const int64_t seg_last_at = last_at_blk[(size_t)nblocks];
-    int64_t np = 0, off_used = 0;
-    auto emit = [&](int64_t output, int64_t input, int bits, int64_t at_pos_abs) -> int {
+    for (; x < text_len; x++) if (text[x] == '@') { cnt++; last = x; }
+    const int64_t seg_at = cnt, seg_last_at = last;
+    int64_t np = 0;
+    auto emit = [&](int64_t output, int64_t input, int bits, int64_t at_abs) -> int {
         if (np >= cap) return -1;
-        p_output[np] = output; p_input[np] = input; p_bits[np] = bits;
-        uint8_t *w = p_window + (size_t)np * 32768;
-        // last 32 KiB of S^T before `output`, zero-filled before the stream start (Index.cs:42-46)
-        for (int64_t i = 0; i < 32768; i++) {
-            int64_t q = output - 32768 + i;
-            w[i] = q < 0 ? 0 : text[q % text_len];
-        }
         int32_t ol = 0;
-        if (at_pos_abs >= 0) {
-            if (output - at_pos_abs > 32768) return -2;
-            ol = (int32_t)(output - at_pos_abs);
-            if (off_used + ol > off_cap) return -1;
-            for (int32_t i = 0; i < ol; i++) p_off[off_used + i] = text[(at_pos_abs + i) % text_len];
+        if (at_abs >= 0) {
+            if (output - at_abs > 32768) return -2;   // C# offset buffer overflow
+            ol = (int32_t)(output - at_abs);
         }
-        p_off_len[np] = ol;
-        off_used += ol;
+        p_output[np] = output; p_input[np] = input; p_bits[np] = bits; p_off_len[np] = ol;
+        p_at[np] = ol ? at_abs : -1;
         np++;
         return 0;
     };
-    // first point right after the gzip header (totout == 0, Core.cs:101-102): no offset bytes
-    if (emit(0, 10, 0, -1) < 0) return -1;
-    int64_t counter_base = 0;  // '@' count at the last point
+    if (emit(0, 10, 0, -1) < 0) return -1;   // right after the gzip header (Core.cs:101-102)
+    int64_t counter_base = 0;                 // '@' count at the last point
     const int64_t seg_bits = seg_gz_len * 8;
-    const int64_t thresh = (int64_t)(uint32_t)(chunksize - 8u);
+    const int64_t thresh = (int64_t)(uint32_t)(chunksize - 8u);   // int > uint compared as long
     for (int64_t r = 0; r < repeats; r++) {
         for (int64_t b = 0; b < nblocks; b++) {
-            int64_t out_abs = r * text_len + out_end[b];
-            int64_t at_abs = r * seg_at + at_blk[b];
-            if (out_abs == 0) {  // a block end before any output also creates a point
-                int64_t bitpos = 80 + r * seg_bits + bit_end[b];
-                int64_t totin = (bitpos + 7) / 8;
+            const int64_t out_abs = r * text_len + out_end[b];
+            const int64_t at_abs = r * seg_at + at_blk[(size_t)b];
+            const int64_t bitpos = 80 + r * seg_bits + bit_end[b];
+            const int64_t totin = (bitpos + 7) / 8;
+            if (out_abs == 0) {
                 int rc = emit(0, totin, (int)(totin * 8 - bitpos), -1);
                 if (rc < 0) return rc;
                 continue;
             }
             if (at_abs - counter_base > thresh) {
-                int64_t bitpos = 80 + r * seg_bits + bit_end[b];
-                int64_t totin = (bitpos + 7) / 8;
                 int64_t last_abs;
-                if (last_at_blk[b] >= 0) last_abs = r * text_len + last_at_blk[b];
+                if (last_at_blk[(size_t)b] >= 0) last_abs = r * text_len + last_at_blk[(size_t)b];
                 else if (r > 0 && seg_last_at >= 0) last_abs = (r - 1) * text_len + seg_last_at;
-                else last_abs = -1;
-                if (last_abs < 0) return -2;  // offset would hold the whole prefix (not our data)
+                else return -2;
                 int rc = emit(out_abs, totin, (int)(totin * 8 - bitpos), last_abs);
                 if (rc < 0) return rc;
                 counter_base = at_abs;
             }
         }
     }
-    // final point at stream end (Core.cs:123): bits 0, input = file length, output = |S|*T
-    int64_t flen = 10 + repeats * seg_gz_len + 10;
-    if (emit(repeats * text_len, flen, 0, -1) < 0) return -1;
+    // the final point at stream end (Core.cs:123): bits 0, input = file length
+    if (emit(repeats * text_len, 10 + repeats * seg_gz_len + 10, 0, -1) < 0) return -1;
     return np;
+}
+
+// Windows (32 KiB each, Index.cs:42-46: the last 32 KiB of S^T before Output, zeros before the
+// start) and offset bytes (concatenated) of points [lo, hi).
+void ppg_synth_tiled_fill(const uint8_t *text, int64_t text_len, const int64_t *p_output, const int32_t *p_off_len,
+                          const int64_t *p_at, int64_t lo, int64_t hi, uint8_t *windows, uint8_t *offsets) {
+    int64_t o = 0;
+    for (int64_t p = lo; p < hi; p++) {
+        uint8_t *w = windows + (p - lo) * 32768;
+        for (int64_t i = 0; i < 32768;) {
+            int64_t q = p_output[p] - 32768 + i;
+            if (q < 0) { w[i++] = 0; continue; }
+            int64_t off = q % text_len, take = std::min<int64_t>(32768 - i, text_len - off);
+            memcpy(w + i, text + off, (size_t)take);
+            i += take;
+        }
+        for (int32_t i = 0; i < p_off_len[p]; i++) offsets[o + i] = text[(p_at[p] + i) % text_len];
+        o += p_off_len[p];
+    }
 }
 
 }  // extern "C"

@@ -1,0 +1,129 @@
+"""Synthetic "tiled" .fastq.gz for the 50 GB configuration (bench input, not the hot path).
+
+One gzip member = header + S_deflate * T + empty final block + trailer, where S is a segment of
+whole Generator-shape records (synth.cpp) deflated pigz-style with no history before it and a
+byte-aligned sync-flush end, so its compressed bytes can be repeated T times; the stream
+decompresses to S^T.  The CreateIndex points of the whole file are derived from the segment's
+deflate block list (ppg_synth_tiled_points), exactly as Core.BuildDeflateIndex (Core.cs:14-131)
+would place them — tests/test_tiled.py checks this against the oracle's serial pass.
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import synth
+from . import Index
+
+
+class TiledFile:
+    def __init__(self, records, repeats, chunksize, read_len=150, seed=0, level=6, piece=4 << 20, threads=16):
+        S = synth()
+        self.records, self.repeats, self.chunksize = records, repeats, chunksize
+        n = S.ppg_synth_fastq_size(0, records, read_len)
+        self.text = np.empty(n, np.uint8)
+        assert S.ppg_synth_fastq(seed, 0, records, read_len, C.c_void_p(self.text.ctypes.data), n, threads) == n
+        cap = n // 2 + (1 << 20)
+        seg = np.empty(cap, np.uint8)
+        crc = C.c_uint32()
+        m = S.ppg_synth_segment(C.c_void_p(self.text.ctypes.data), n, level, piece, threads,
+                                C.c_void_p(seg.ctypes.data), cap, C.byref(crc))
+        assert m > 0
+        self.seg = seg[:m].copy()
+        self.seg_crc = crc.value
+        self.header = np.zeros(10, np.uint8)
+        self.tail = np.zeros(10, np.uint8)
+        S.ppg_synth_tiled_frame(self.seg_crc, n, repeats, C.c_void_p(self.header.ctypes.data),
+                                C.c_void_p(self.tail.ctypes.data))
+        self.file_len = 10 + repeats * m + 10
+        # deflate block ends of the segment
+        bcap = m // 16 + 1024
+        be, oe = np.empty(bcap, np.int64), np.empty(bcap, np.int64)
+        nb = S.ppg_synth_segment_blocks(C.c_void_p(self.seg.ctypes.data), m, n, C.c_void_p(be.ctypes.data),
+                                        C.c_void_p(oe.ctypes.data), bcap)
+        assert 0 < nb <= bcap
+        self.block_bit_end, self.block_out_end = be[:nb].copy(), oe[:nb].copy()
+        # point metadata for the whole member (windows/offsets are filled per range: windows())
+        pcap = (records * repeats) // max(1, chunksize - 8) + 64
+        pcap = min(pcap, nb * repeats + 2)
+        out, inp = np.empty(pcap, np.int64), np.empty(pcap, np.int64)
+        bits, ol, at = np.empty(pcap, np.int32), np.empty(pcap, np.int32), np.empty(pcap, np.int64)
+        npts = S.ppg_synth_tiled_points(C.c_void_p(self.text.ctypes.data), n, m, repeats,
+                                        C.c_void_p(self.block_bit_end.ctypes.data),
+                                        C.c_void_p(self.block_out_end.ctypes.data), nb, chunksize & 0xFFFFFFFF,
+                                        C.c_void_p(out.ctypes.data), C.c_void_p(inp.ctypes.data),
+                                        C.c_void_p(bits.ctypes.data), C.c_void_p(ol.ctypes.data),
+                                        C.c_void_p(at.ctypes.data), pcap)
+        assert npts > 0, npts
+        self.p_output, self.p_input, self.p_bits = out[:npts].copy(), inp[:npts].copy(), bits[:npts].copy()
+        self.p_offlen, self._p_at = ol[:npts].copy(), at[:npts].copy()
+        self.npoints = int(npts)
+
+    def windows(self, lo=0, hi=None):
+        """(windows uint8[(hi-lo)*32768], offsets uint8[...]) of points [lo, hi)."""
+        if hi is None:
+            hi = self.npoints
+        win = np.empty((hi - lo) * 32768, np.uint8)
+        offs = np.empty(max(1, int(self.p_offlen[lo:hi].sum())), np.uint8)
+        synth().ppg_synth_tiled_fill(C.c_void_p(self.text.ctypes.data), self.text.size,
+                                     C.c_void_p(self.p_output.ctypes.data), C.c_void_p(self.p_offlen.ctypes.data),
+                                     C.c_void_p(self._p_at.ctypes.data), lo, hi, C.c_void_p(win.ctypes.data),
+                                     C.c_void_p(offs.ctypes.data))
+        return win, offs[: int(self.p_offlen[lo:hi].sum())]
+
+    @property
+    def text_len(self):
+        return self.text.size
+
+    def index(self, lo=0, hi=None):
+        """Index (libppgpu) of points [lo, hi): chunks lo..hi-2 of the member."""
+        if hi is None:
+            hi = self.npoints
+        win, offs = self.windows(lo, hi)
+        return Index.from_points(self.p_output[lo:hi], self.p_input[lo:hi], self.p_bits[lo:hi], win,
+                                 self.p_offlen[lo:hi], offs)
+
+    def file_bytes(self, lo=0, hi=None):
+        """Bytes [lo, hi) of the tiled file (host copy; for tests and the CPU baseline sample)."""
+        if hi is None:
+            hi = self.file_len
+        out = np.empty(hi - lo, np.uint8)
+        m = self.seg.size
+        pos = lo
+        while pos < hi:
+            if pos < 10:
+                take = min(hi, 10) - pos
+                out[pos - lo:pos - lo + take] = self.header[pos:pos + take]
+            elif pos < 10 + self.repeats * m:
+                off = (pos - 10) % m
+                take = min(hi - pos, m - off)
+                out[pos - lo:pos - lo + take] = self.seg[off:off + take]
+            else:
+                off = pos - 10 - self.repeats * m
+                take = hi - pos
+                out[pos - lo:pos - lo + take] = self.tail[off:off + take]
+            pos += take
+        return out
+
+    def fill_device(self, dst, lo, hi):
+        """Write file bytes [lo, hi) into the uint8 torch tensor dst (on a GPU) by device copies
+        of the segment: the 50 GB member never exists in host memory."""
+        import torch
+        dev = dst.device
+        seg = torch.from_numpy(self.seg).to(dev)
+        hdr = torch.from_numpy(self.header).to(dev)
+        tail = torch.from_numpy(self.tail).to(dev)
+        m = self.seg.size
+        pos = lo
+        while pos < hi:
+            if pos < 10:
+                take = min(hi, 10) - pos
+                dst[pos - lo:pos - lo + take].copy_(hdr[pos:pos + take])
+            elif pos < 10 + self.repeats * m:
+                off = (pos - 10) % m
+                take = min(hi - pos, m - off)
+                dst[pos - lo:pos - lo + take].copy_(seg[off:off + take])
+            else:
+                off = pos - 10 - self.repeats * m
+                take = hi - pos
+                dst[pos - lo:pos - lo + take].copy_(tail[off:off + take])
+            pos += take

@@ -1,0 +1,40 @@
+"""The bench's tiled 50 GB construction, checked at small scale: the file is a valid single gzip
+member (Python's gzip + trailer), and the CreateIndex points derived from the segment's block
+list equal the oracle's serial Core.BuildDeflateIndex pass over the materialised file."""
+import gzip
+import hashlib
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from parallelparsing_amd.tiled import TiledFile
+
+
+@pytest.mark.parametrize("records,repeats,chunk,piece", [(3000, 5, 1000, 1 << 18), (2500, 7, 333, 1 << 20),
+                                                          (1200, 3, 10000, 1 << 16)])
+def test_tiled_points_equal_oracle(records, repeats, chunk, piece):
+    tf = TiledFile(records, repeats, chunk, piece=piece, threads=4)
+    f = tf.file_bytes().tobytes()
+    assert len(f) == tf.file_len
+    text = gzip.decompress(f)
+    assert text == tf.text.tobytes() * repeats
+    assert int.from_bytes(f[-8:-4], "little") == zlib.crc32(text)
+    oi = O.build_index(f, chunk)
+    pts = oi.points()
+    assert len(pts) == tf.npoints
+    win, offs = tf.windows()
+    off = 0
+    for i, (o, n, b, w, offset) in enumerate(pts):
+        assert (o, n, b) == (tf.p_output[i], tf.p_input[i], tf.p_bits[i]), i
+        assert w == win[i * 32768:(i + 1) * 32768].tobytes(), i
+        ol = int(tf.p_offlen[i])
+        assert offset == offs[off:off + ol].tobytes(), i
+        off += ol
+    # a sub-range fill equals the same slice of the full fill
+    lo, hi = 1, max(2, tf.npoints - 1)
+    w2, o2 = tf.windows(lo, hi)
+    assert w2.tobytes() == win[lo * 32768:hi * 32768].tobytes()
+    s0 = int(tf.p_offlen[:lo].sum())
+    assert o2.tobytes() == offs[s0:s0 + len(o2)].tobytes()
