@@ -156,7 +156,7 @@ def main():
         total_records = int(counts.sum())
     else:
         total_records = local_records
-    expect = tf.records * tf.repeats
+    expect = tf.expected_records()   # includes the reference's Q1 duplicates
     assert total_records == expect, (total_records, expect)
 
     text_bytes = int(ix_out[-1] - ix_out[0])

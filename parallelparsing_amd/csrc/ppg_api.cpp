@@ -333,7 +333,7 @@ const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    int ring_bits = 14;   // inflate history ring: 2^13..2^15 bytes of LDS per wavefront
+    int ring_bits = 13;   // inflate history ring: 2^13..2^15 bytes of LDS per wavefront
 };
 
 namespace {

@@ -58,6 +58,19 @@ class TiledFile:
         self.p_offlen, self._p_at = ol[:npts].copy(), at[:npts].copy()
         self.npoints = int(npts)
 
+    def expected_records(self):
+        """Records DecompressAll emits for the whole member: every record once, plus one duplicate
+        per Point that falls exactly on a record start (its offset then holds the whole previous
+        record, which the next chunk parses again: SURVEY Q1, Core.cs:86-94 + Parsing.cs:11-51)."""
+        dup = 0
+        tl = self.text.size
+        for p in np.nonzero(self.p_offlen)[0]:
+            a = int(self._p_at[p]) % tl
+            n = int(self.p_offlen[p])
+            seg = self.text[a:a + n] if a + n <= tl else np.concatenate([self.text[a:], self.text[:a + n - tl]])
+            dup += int(np.count_nonzero(seg == 10) == 4)
+        return self.records * self.repeats + dup
+
     def windows(self, lo=0, hi=None):
         """(windows uint8[(hi-lo)*32768], offsets uint8[...]) of points [lo, hi)."""
         if hi is None:

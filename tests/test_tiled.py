@@ -13,7 +13,7 @@ from parallelparsing_amd.tiled import TiledFile
 
 
 @pytest.mark.parametrize("records,repeats,chunk,piece", [(3000, 5, 1000, 1 << 18), (2500, 7, 333, 1 << 20),
-                                                          (1200, 3, 10000, 1 << 16)])
+                                                          (1200, 3, 10000, 1 << 16), (4000, 9, 40, 1 << 17)])
 def test_tiled_points_equal_oracle(records, repeats, chunk, piece):
     tf = TiledFile(records, repeats, chunk, piece=piece, threads=4)
     f = tf.file_bytes().tobytes()
@@ -32,6 +32,9 @@ def test_tiled_points_equal_oracle(records, repeats, chunk, piece):
         ol = int(tf.p_offlen[i])
         assert offset == offs[off:off + ol].tobytes(), i
         off += ol
+    # DecompressAll's record count (duplicates at record-aligned Points included)
+    tot, _ = O.decompress_all(f, oi, threads=4)
+    assert tot == tf.expected_records()
     # a sub-range fill equals the same slice of the full fill
     lo, hi = 1, max(2, tf.npoints - 1)
     w2, o2 = tf.windows(lo, hi)
