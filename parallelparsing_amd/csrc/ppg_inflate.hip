@@ -39,22 +39,23 @@ struct __attribute__((aligned(16))) InflateLds {
     uint8_t lens[320];
 };
 
+// v_writelane_b32 (value, lane, old) — the LLVM intrinsic, not exposed as a clang builtin
+extern "C" __device__ int llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane");
+
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 
-// Compressed stream of one chunk: word i (chunk-relative) is base[i].  128 words live across the
-// lanes (lane l holds words wb+2l in A and wb+2l+1 in B), so a refill is one v_readlane.  The
-// buffer is reloaded with ONE global_load_dwordx2 per lane whose result is used at once: the
-// wait (~one memory latency per 512 B of input, ~280 symbols) is paid there and nowhere else.
-// A load whose result stayed in flight across loop iterations would make the compiler wait for
-// every outstanding memory operation at each use (its per-register tracking is conservative
-// around loops), and an untracked asm load can be copied by the register allocator before it
-// lands.
+// Compressed stream of one chunk: word i (chunk-relative) is base[i].  256 words live across the
+// lanes (lane l holds word wb+l in A and wb+64+l in B), so fetching stream words is v_readlane.
+// A reload is two coalesced dword loads per lane whose results are consumed at once: the wait
+// (~one memory latency per ~500 B of input) is paid there and nowhere else.  A load whose result
+// stayed in flight across loop iterations would make the compiler wait for every outstanding
+// memory operation at each use (including the output flush stores).
 struct Reader {
-    const uint32_t *base;   // 128-word aligned
+    const uint32_t *base;
     uint32_t nw;            // readable words from base (>= 1)
-    uint32_t A, B;          // words wb+2*lane, wb+2*lane+1
+    uint32_t A, B;          // words wb+lane, wb+64+lane
     uint32_t wb;            // first word of the buffer
     uint32_t wi;            // next word to append to bb
     uint64_t bb;            // bit buffer, LSB = next bit
@@ -62,28 +63,25 @@ struct Reader {
 };
 
 __device__ __forceinline__ void rd_load(Reader &r, int lane) {
-    const uint32_t i = r.wb + 2 * lane;
-    if (i + 1 < r.nw) {
-        const uint2 v = *(const uint2 *)(r.base + i);   // 8-B aligned: wb and base are
-        r.A = v.x;
-        r.B = v.y;
-    } else {
-        r.A = i < r.nw ? r.base[i] : 0u;   // past the end: zeros (an overrun is an error anyway)
-        r.B = 0u;
-    }
-    // consume the load here, so the compiler waits for it in this (rare) block rather than at
-    // every v_readlane of A/B (there the wait would drain every store in flight, too)
+    const uint32_t i = r.wb + lane;
+    r.A = i < r.nw ? r.base[i] : 0u;          // past the end: zeros (an overrun is an error anyway)
+    r.B = i + 64 < r.nw ? r.base[i + 64] : 0u;
+    // consume the loads here, so the compiler waits for them in this (rare) block rather than
+    // at every v_readlane of A/B (there the wait would drain every store in flight, too)
     asm volatile("" ::"v"(r.A), "v"(r.B));
 }
 
 __device__ __forceinline__ uint32_t rd_word(const Reader &r, uint32_t idx) {
-    return (idx & 1) ? rdlane(r.B, idx >> 1) : rdlane(r.A, idx >> 1);
+    return idx < 64 ? rdlane(r.A, idx) : rdlane(r.B, idx - 64);
 }
 
+// position the bit buffer at chunk-relative bit `bit` (reloads only when outside the buffer)
 __device__ __forceinline__ void rd_seek(Reader &r, uint32_t bit, int lane) {
     r.wi = bit >> 5;
-    r.wb = r.wi & ~127u;
-    rd_load(r, lane);
+    if (r.wi < r.wb || r.wi >= r.wb + 128) {
+        r.wb = r.wi;
+        rd_load(r, lane);
+    }
     const uint32_t w = rd_word(r, r.wi - r.wb);
     r.wi++;
     const uint32_t sh = bit & 31;
@@ -94,8 +92,8 @@ __device__ __forceinline__ void rd_seek(Reader &r, uint32_t bit, int lane) {
 // guarantees bn >= 32
 __device__ __forceinline__ void rd_refill(Reader &r, int lane) {
     if (r.bn <= 32) {
-        if (r.wi == r.wb + 128) {
-            r.wb += 128;
+        if (r.wi >= r.wb + 128) {
+            r.wb = r.wi;
             rd_load(r, lane);
         }
         const uint32_t w = rd_word(r, r.wi - r.wb);
@@ -150,6 +148,55 @@ __device__ __forceinline__ void flush_range(const uint8_t *ring, uint8_t *out, u
     }
 }
 
+// Byte at chunk position p older than the ring: the flushed output (p >= 0) or the Point's window.
+// Read as an aligned dword so the compiler never merges it with an LDS byte load into one flat load.
+__device__ __forceinline__ uint32_t far_byte(const uint8_t *out, const uint8_t *dict, uint64_t out_off, int32_t p) {
+    const uint8_t *a = p >= 0 ? out + out_off + (uint32_t)p : dict + 32768 + p;   // p >= -32768
+    const uint32_t w = *(const uint32_t *)((uintptr_t)a & ~(uintptr_t)3);
+    return (w >> (8 * ((uintptr_t)a & 3))) & 255u;
+}
+
+// One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
+template <int RB>
+__device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, const uint8_t *dict, uint64_t out_off,
+                                           uint32_t rb0, uint32_t pos, uint32_t dist, uint32_t n, int lane) {
+    constexpr uint32_t RING = 1u << RB;
+    constexpr uint32_t RM = RING - 1;
+    const uint32_t dst0 = rb0 + pos;   // ring slot of the first output byte
+    if (dist + n <= RING) {
+        // source entirely in the ring and never overwritten by this copy; every source byte
+        // precedes pos, so no 64-byte group reads another group's output
+        const uint32_t src0 = dst0 - dist;
+        if (dist >= n) {
+            for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                if (j < n) ring[(dst0 + j) & RM] = ring[(src0 + j) & RM];
+            }
+        } else {
+            // overlapping run: byte j repeats byte j mod dist
+            for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                if (j < n) ring[(dst0 + j) & RM] = ring[(src0 + j % dist) & RM];
+            }
+        }
+    } else {
+        // far reference (dist > RING - n >= n): bytes older than the ring come from the flushed
+        // output (this wave's own earlier stores: same-wave accesses to an address are ordered)
+        // or the Point's window
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            if (j < n) {
+                const uint32_t back = dist - j;                 // source = pos - back
+                const int32_t rel = (int32_t)pos - (int32_t)back;
+                uint32_t v;
+                if (back + n <= RING) v = ring[(dst0 - back) & RM];
+                else v = far_byte(out, dict, out_off, rel);
+                ring[(dst0 + j) & RM] = (uint8_t)v;
+            }
+        }
+    }
+}
+
 template <int RB>
 __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
@@ -182,6 +229,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     // chunk-relative compressed stream
     const uint64_t w0abs = (J.bit_start >> 5) & ~127ull;
     Reader r;
+    r.wb = 0x80000000u;   // empty buffer: the first seek loads
     r.base = comp + w0abs;
     r.nw = (uint32_t)min(nwords > w0abs ? nwords - w0abs : 1ull, 0xFFFFFFFFull);
     const uint32_t bit_limit = (uint32_t)min(J.bit_limit - w0abs * 32, 0xFFFFFFFFull);
@@ -192,8 +240,6 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     uint32_t fl_next = UNIT - (uint32_t)(out_off & (UNIT - 1));   // next global 4 KiB boundary
     int status = ST_OK, flags = 0, last = 0, in_block = 0;
     uint32_t vlit = 0, vdst = 0;    // first-level tables (one entry per lane)
-    uint32_t pv = 0;                // deferred match bytes (one per lane) ...
-    uint32_t ppos = 0, pn = 0;      // ... for ring slots [ppos, ppos + pn)
 
     while (pos < len && !last) {
         r.wb = uni(r.wb);
@@ -305,83 +351,161 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         pos = uni(pos);
         fl_done = uni(fl_done);
         fl_next = uni(fl_next);
-        pn = 0;
 
-        // ---- token loop: everything below is wave-uniform (scalar branches) ----
+        // ---- token rounds ----
+        // Speculative lane-parallel decode: every lane decodes one whole token (litlen code, length
+        // extra bits, distance code, distance extra bits) as if a token started at bit bp + lane.
+        // A scalar walk then follows the real chain of tokens (start, start + bits, ...) through
+        // the lanes, emitting each one, until the chain leaves the 64-bit span; the next round
+        // starts where it left.  Codes longer than the root tables, end-of-block and invalid codes
+        // stop the walk and are decoded by the bit-serial path below.
+        uint32_t bp = rd_pos(r);
         while (pos < len) {
-            rd_refill(r, lane);
-            const uint32_t e = lookup(vlit, S.lit, (1u << LB) - 1, r, S.lit_count, S.lit_sorted, TAB_LIT);
-            br_take(r, e & 15);
-            const uint32_t kind = (e >> 4) & 3;
-            if (kind == K_LIT) {
-                if (pn) { if ((uint32_t)lane < pn) S.ring[(ppos + lane) & RM] = (uint8_t)pv; pn = 0; }
-                if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)(e >> 8);
-                pos++;
-            } else if (kind == K_BASE) {
-                const uint32_t mlen = (e >> 16) + br_take(r, (e >> 8) & 15);
-                rd_refill(r, lane);
-                const uint32_t d = lookup(vdst, S.dst, (1u << DB) - 1, r, S.dst_count, S.dst_sorted, TAB_DST);
-                br_take(r, d & 15);
-                if (((d >> 4) & 3) != K_BASE) { status = ST_DATA_ERROR; break; }
-                const uint32_t dist = (d >> 16) + br_take(r, (d >> 8) & 15);
-                const uint32_t n = min(mlen, len - pos);
-                if (pn) { if ((uint32_t)lane < pn) S.ring[(ppos + lane) & RM] = (uint8_t)pv; pn = 0; }
-                const uint32_t dst0 = rb0 + pos;          // ring slot of the first output byte
-                if (dist + n <= RING) {
-                    // source entirely in the ring and never overwritten by this copy; every
-                    // source byte precedes pos, so no 64-byte group reads another's output.  The
-                    // last group's write is deferred: its LDS read overlaps the next decode.
-                    const uint32_t src0 = dst0 - dist;
-                    uint32_t j0 = 0;
-                    if (dist >= n) {
-                        for (; j0 + 64 < n; j0 += 64) {
-                            const uint8_t v = S.ring[(src0 + j0 + lane) & RM];
-                            S.ring[(dst0 + j0 + lane) & RM] = v;
-                        }
-                        if (j0 + lane < n) pv = S.ring[(src0 + j0 + lane) & RM];
-                    } else {
-                        // overlapping run: byte j repeats byte j mod dist
-                        for (; j0 + 64 < n; j0 += 64) {
-                            const uint8_t v = S.ring[(src0 + (j0 + lane) % dist) & RM];
-                            S.ring[(dst0 + j0 + lane) & RM] = v;
-                        }
-                        if (j0 + lane < n) pv = S.ring[(src0 + (j0 + lane) % dist) & RM];
-                    }
-                    ppos = dst0 + j0;
-                    pn = n - j0;
-                } else {
-                    // far reference (dist > RING - n >= n): bytes older than the ring come from
-                    // the flushed output or the Point's window; the flush stores complete first
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-                        const uint32_t j = j0 + lane;
-                        if (j < n) {
-                            const uint32_t back = dist - j;                 // source = pos - back
-                            const int32_t rel = (int32_t)pos - (int32_t)back;
-                            uint8_t v;
-                            if (back + n <= RING) v = S.ring[(dst0 - back) & RM];
-                            else if (rel >= 0) v = out[out_off + (uint32_t)rel];
-                            else v = dict[32768 + rel];                    // rel >= -32768
-                            S.ring[(dst0 + j) & RM] = v;
-                        }
-                    }
+            const uint32_t wq = bp >> 5;
+            if (wq < r.wb || wq + 4 >= r.wb + 128) {
+                r.wb = wq;
+                rd_load(r, lane);
+            }
+            const uint32_t wi = wq - r.wb;
+            uint32_t w0, w1, w2, w3, w4;
+            if (wi + 4 < 64) {
+                w0 = rdlane(r.A, wi); w1 = rdlane(r.A, wi + 1); w2 = rdlane(r.A, wi + 2);
+                w3 = rdlane(r.A, wi + 3); w4 = rdlane(r.A, wi + 4);
+            } else if (wi >= 64) {
+                w0 = rdlane(r.B, wi - 64); w1 = rdlane(r.B, wi - 63); w2 = rdlane(r.B, wi - 62);
+                w3 = rdlane(r.B, wi - 61); w4 = rdlane(r.B, wi - 60);
+            } else {
+                w0 = rd_word(r, wi); w1 = rd_word(r, wi + 1); w2 = rd_word(r, wi + 2);
+                w3 = rd_word(r, wi + 3); w4 = rd_word(r, wi + 4);
+            }
+            // 64 stream bits at bp + lane
+            const uint32_t o = (bp & 31) + (uint32_t)lane;   // 0..94
+            const uint32_t kq = o >> 5, sh = o & 31;
+            const uint32_t x0 = kq == 0 ? w0 : (kq == 1 ? w1 : w2);
+            const uint32_t x1 = kq == 0 ? w1 : (kq == 1 ? w2 : w3);
+            const uint32_t x2 = kq == 0 ? w2 : (kq == 1 ? w3 : w4);
+            const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, sh);
+            const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, sh);
+            // litlen symbol + length extra bits
+            const uint32_t e = S.lit[lo & ((1u << LB) - 1)];
+            const uint32_t L = e & 15, kind = (e >> 4) & 3;
+            const bool islen = kind == K_BASE;
+            const uint64_t xs = ((((uint64_t)hi) << 32) | lo) >> L;
+            const uint32_t xb = islen ? (e >> 8) & 15 : 0u;
+            const uint32_t mlen = (e >> 16) + ((uint32_t)xs & ((1u << xb) - 1));
+            // distance symbol + extra bits (harmless garbage on literal lanes)
+            const uint32_t y = (uint32_t)(xs >> xb);
+            const uint32_t d = S.dst[y & ((1u << DB) - 1)];
+            const uint32_t L2 = d & 15, xd = (d >> 8) & 15;
+            const uint32_t dist = (d >> 16) + ((y >> L2) & ((1u << xd) - 1));
+            const bool special = L == 0 || kind >= K_EOB || (islen && (L2 == 0 || ((d >> 4) & 3) != K_BASE));
+            const uint32_t tb = islen ? L + xb + L2 + xd : L;
+            // token word: [6:0] lane of the next token, [31:23] output bytes; a special token is
+            // 0xFF | lane << 8 (next lane 127 ends the walk, 0 bytes)
+            const uint32_t vtok = special ? (0xFFu | ((uint32_t)lane << 8))
+                                          : (((uint32_t)lane + tb) | ((islen ? mlen : 1u) << 23));
+            // token info: [31] match, [15:0] distance (match) or the literal byte
+            const uint32_t vinf = islen ? (0x80000000u | dist) : ((e >> 8) & 255);
+
+            // ---- walk the real token chain (wave-uniform): lane s -> lane s + bits(s) ----
+            // Records each token's info at the lane of its output offset (vtin) and the offsets in
+            // the mask mo; stops when the chain leaves the 64-bit span, at a special token (which
+            // is recorded with 0 bytes, harmlessly), or once no further token can start inside
+            // the first lim output bytes of the round.
+            const uint32_t lim = min(64u, len - pos);
+            const uint32_t cl = 64u - lim;   // off < lim  <=>  off + cl < 64
+            uint32_t s = 0, off = 0, t;
+            uint64_t mo = 0;
+            uint32_t vtin = 0;
+            do {
+                t = rdlane(vtok, s);
+                mo |= 1ull << off;
+                vtin = (uint32_t)llvm_writelane((int)rdlane(vinf, s), (int)off, (int)vtin);
+                off += t >> 23;
+                s = t & 127u;
+            } while (max(s, off + cl) < 64u);
+            const bool spec = (t & 0x80u) != 0;
+            if (spec) s = (t >> 8) & 63u;
+            const uint32_t rout = min(off, len - pos);   // output bytes of this round
+
+            // ---- emit the round's first 64 output bytes, one per lane ----
+            {
+                const uint32_t j = (uint32_t)lane;
+                const uint64_t mle = j == 63 ? ~0ull : ((2ull << j) - 1ull);   // lanes <= j
+                const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & mle);   // start of j's token (bit 0 of mo is set)
+                const uint32_t inf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sj << 2), (int)vtin);
+                const bool act = j < rout;
+                const bool ism = (inf >> 31) != 0;
+                const int32_t jj = (int32_t)j - (int32_t)(inf & 0xFFFFu);   // source, relative to the round
+                const bool dep = act && ism && jj >= 0;                      // produced in this round
+                uint32_t val = inf & 255u;
+                if (act && ism && jj < 0 && jj >= -(int32_t)RING) val = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                const bool far = act && ism && jj < -(int32_t)RING;
+                if (__ballot(far)) {
+                    if (far) val = far_byte(out, dict, out_off, (int32_t)pos + jj);
                 }
+                if (__ballot(dep)) {
+                    // chains inside the round (short distances): pointer doubling to a resolved byte
+                    int32_t ptr = dep ? jj : (int32_t)j;
+                    for (;;) {
+                        const int32_t p2 = __builtin_amdgcn_ds_bpermute(ptr << 2, ptr);
+                        if (!__ballot(p2 != ptr)) break;
+                        ptr = p2;
+                    }
+                    val = (uint32_t)__builtin_amdgcn_ds_bpermute(ptr << 2, (int)val);
+                }
+                if (act) S.ring[(rb0 + pos + j) & RM] = (uint8_t)val;
+            }
+            if (rout > 64) {
+                // the rest of the last token (a match): bytes 64.. of the round
+                const uint32_t last = 63u - (uint32_t)__builtin_clzll(mo);
+                const uint32_t dl = rdlane(vtin, last) & 0xFFFFu;
+                copy_match<RB>(S.ring, out, dict, out_off, rb0, pos + 64, dl, rout - 64, lane);
+            }
+            pos += rout;
+            if (pos >= fl_next) {
+                flush_range<RB>(S.ring, out, out_off + fl_done, out_off + fl_next, lane);
+                fl_done = fl_next;
+                fl_next += UNIT;
+            }
+            bp += s;
+            if (!spec) continue;
+
+            // ---- one token by the bit-serial path (long code, end-of-block or error) ----
+            rd_seek(r, bp, lane);
+            rd_refill(r, lane);
+            const uint32_t e1 = lookup(vlit, S.lit, (1u << LB) - 1, r, S.lit_count, S.lit_sorted, TAB_LIT);
+            br_take(r, e1 & 15);
+            const uint32_t kind1 = (e1 >> 4) & 3;
+            if (kind1 == K_LIT) {
+                if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)(e1 >> 8);
+                pos++;
+            } else if (kind1 == K_BASE) {
+                const uint32_t ml = (e1 >> 16) + br_take(r, (e1 >> 8) & 15);
+                rd_refill(r, lane);
+                const uint32_t d1 = lookup(vdst, S.dst, (1u << DB) - 1, r, S.dst_count, S.dst_sorted, TAB_DST);
+                br_take(r, d1 & 15);
+                if (((d1 >> 4) & 3) != K_BASE) { status = ST_DATA_ERROR; break; }
+                const uint32_t ds = (d1 >> 16) + br_take(r, (d1 >> 8) & 15);
+                const uint32_t n = min(ml, len - pos);
+                copy_match<RB>(S.ring, out, dict, out_off, rb0, pos, ds, n, lane);
                 pos += n;
-            } else if (kind == K_EOB) {
+            } else if (kind1 == K_EOB) {
                 in_block = 0;
+                bp = rd_pos(r);
                 break;
             } else {
                 status = ST_DATA_ERROR;
                 break;
             }
+            bp = rd_pos(r);
             if (pos >= fl_next) {
-                if (pn) { if ((uint32_t)lane < pn) S.ring[(ppos + lane) & RM] = (uint8_t)pv; pn = 0; }
                 flush_range<RB>(S.ring, out, out_off + fl_done, out_off + fl_next, lane);
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
         }
-        if (pn) { if ((uint32_t)lane < pn) S.ring[(ppos + lane) & RM] = (uint8_t)pv; pn = 0; }
+        if (status == ST_OK) rd_seek(r, bp, lane);   // the next block header / the R-E5 check read from bp
         if (status != ST_OK) break;
     }
     flush_range<RB>(S.ring, out, out_off + fl_done, out_off + pos, lane);
