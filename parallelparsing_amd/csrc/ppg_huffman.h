@@ -4,17 +4,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define LB 10            // litlen root table bits
+#define LB 9             // litlen root table bits (codes <= 9 bits: 99.9% of FASTQ tokens)
 #define DB 8             // distance root table bits
 #define CB 7             // code-length-code table bits (complete: max code length is 7)
-#define UNIT 4096        // flush unit (bytes, global-address aligned)
 
-// table entry: [3:0] code length (0 = slow path) [5:4] kind [15:8] literal / extra bits [31:16] base
-#define K_LIT 0u
-#define K_BASE 1u
-#define K_EOB 2u
-#define K_BAD 3u
-
+// Root-table entries (the lane-parallel decoder's format).  Every field is placed so that one
+// VALU op extracts or applies it: bits [4:0] are the code length (bit 4 always 0), so
+// v_alignbit / v_lshrrev consume the code straight from the entry.
+//  litlen: [3:0] code length L, 0 = decode bit-serially (end-of-block, invalid symbol, or a code
+//          longer than the root table), [9:5] L + length extra bits, [14:10] length extra bits,
+//          [15] length symbol, [31:16] literal byte or length base
+//  dist:   [3:0] L2 (0 = bit-serial), [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base
+//  code-length code: [3:0] L, [15:8] symbol
 
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
                                      35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -34,17 +35,18 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int kind) {
     if (kind == TAB_CL) return len | (sym << 8);
     if (kind == TAB_LIT) {
-        if (sym < 256) return len | (K_LIT << 4) | (sym << 8);
-        if (sym == 256) return len | (K_EOB << 4);
-        if (sym < 286) return len | (K_BASE << 4) | ((uint32_t)c_lext[sym - 257] << 8) | ((uint32_t)c_lbase[sym - 257] << 16);
-        return len | (K_BAD << 4);
+        if (sym < 256) return len | (len << 5) | (sym << 16);
+        if (sym == 256 || sym >= 286) return 0u;
+        const uint32_t x = c_lext[sym - 257];
+        return len | ((len + x) << 5) | (x << 10) | 0x8000u | ((uint32_t)c_lbase[sym - 257] << 16);
     }
-    if (sym < 30) return len | (K_BASE << 4) | ((uint32_t)c_dext[sym] << 8) | ((uint32_t)c_dbase[sym] << 16);
-    return len | (K_BAD << 4);
+    if (sym >= 30) return 0u;
+    const uint32_t x = c_dext[sym];
+    return len | ((len + x) << 5) | (x << 10) | ((uint32_t)c_dbase[sym] << 16);
 }
 
 // Builds a canonical-Huffman root table of 2^TB entries from n code lengths (all 64 lanes).
-// Codes longer than TB (and unused patterns of an incomplete code) get entry 0 -> slow path,
+// Codes longer than TB (and unused patterns of an incomplete code) get entry 0 -> bit-serial path,
 // which decodes bit-by-bit from count[]/sorted[].  Validity follows zlib 1.2.11 inflate_table:
 // over-subscribed -> error; incomplete -> error unless exactly one code of length 1 (not for
 // the code-length code); no codes at all -> accepted (decoding then fails).  Returns 0 / -1.
@@ -102,11 +104,15 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t
     for (int e0 = 0; e0 < (1 << TB); e0 += 64) {   // uniform trip count (see ppg_inflate_kernel)
         const int e = e0 + lane;
         uint32_t code = 0, first = 0, index = 0, entry = 0;
+        bool found = false;
 #pragma unroll
         for (int l = 1; l <= TB; l++) {
             code |= ((uint32_t)e >> (l - 1)) & 1u;
             uint32_t c = cnt[l];
-            if (entry == 0 && code - first < c) entry = make_entry(sorted[index + code - first], (uint32_t)l, kind);
+            if (!found && code - first < c) {
+                entry = make_entry(sorted[index + code - first], (uint32_t)l, kind);
+                found = true;
+            }
             index += c;
             first = (first + c) << 1;
             code <<= 1;
@@ -145,14 +151,6 @@ __device__ int slow_decode(R &b, const uint16_t *count, const uint16_t *sorted) 
         code <<= 1;
     }
     return -1;
-}
-
-// Slow path as a table entry (length field 0: the code is already consumed); K_BAD if invalid.
-template <class R>
-__device__ __forceinline__ uint32_t slow_entry(R &b, const uint16_t *count, const uint16_t *sorted, int kind) {
-    const int sym = slow_decode(b, count, sorted);
-    if (sym < 0) return K_BAD << 4;
-    return uni(make_entry((uint32_t)sym, 0, kind));
 }
 
 // status codes (ZResult, Interop/Conventions.cs:9-20)

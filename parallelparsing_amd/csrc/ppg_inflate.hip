@@ -5,21 +5,24 @@
 // inflate(Z_NO_FLUSH) until to.Output - from.Output bytes exist.  One 64-lane wavefront decodes
 // one chunk; chunks are independent because every Point carries its 32 KiB history.
 //
-// Where the time goes on gfx950 (measured, scratch micro-benchmarks, 2.39 GHz): a dependent
-// uniform ds_read + v_readfirstlane costs ~92 cycles, an s_load hit ~52, a dependent SALU op
-// ~6-8.  Inflate is a serial chain of such steps per chunk, so the kernel is built to keep the
-// chain short and to fit many wavefronts per CU:
-//   * decoder state (bit buffer, positions) is wave-uniform in SGPRs; every branch is scalar;
-//   * the compressed stream sits in two VGPRs (128 words across the lanes, refilled 256 B at a
-//     time by coalesced loads issued a buffer ahead) and is read with v_readlane -> no memory
-//     wait on the bit-buffer refill;
-//   * 6-bit first-level litlen/distance tables live in one VGPR each (v_readlane, ~90% of
-//     symbols); the full 10/8-bit root tables and the bit-serial slow path sit in LDS;
-//   * history is an LDS ring of 2^RB bytes (8-16 KiB -> 7-11 waves per CU) indexed by the
-//     GLOBAL output address; back-references further than the ring read the already flushed
-//     output (or the Point's window) from HBM;
-//   * a match's LDS read is left in flight while the next symbol decodes (deferred write);
-//   * completed 4 KiB units leave the ring as 16-B-per-lane coalesced stores.
+// DEFLATE is a serial bit stream, and a single wave issues roughly one instruction per ~8
+// cycles on gfx950, so the kernel is organised to need few instructions per token and to keep
+// many waves per CU:
+//   * speculative lane-parallel decode: in each round every lane decodes one whole token
+//     (litlen code, length extra bits, distance code, distance extra bits) as if a token
+//     started at bit bp + lane, using 10/8-bit LDS root tables whose entries are laid out for
+//     single-op extraction; a scalar walk then follows the real chain of tokens through the
+//     lanes (lane s -> lane s + bits(s)), recording each token at its output offset;
+//   * byte-parallel emit: each lane produces one output byte of the round (its token found by
+//     mask + clz, the token's info fetched with ds_bpermute); sources inside the round are
+//     resolved by pointer doubling, so one ds_write commits up to 64 bytes;
+//   * codes longer than the root tables, end-of-block and invalid codes end the walk and are
+//     decoded bit-serially (canonical decode from the per-length counts);
+//   * the compressed stream streams into an LDS ring by global_load_lds (two segments ahead) and
+//     lanes read their words from it directly;
+//   * history is an LDS ring of 2^RB bytes (4-32 KiB) indexed by the GLOBAL output
+//     address; references further back read the already flushed output (or the Point's window)
+//     from HBM; completed 4 KiB units leave the ring as 16-B-per-lane coalesced stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "ppg_device.h"
@@ -28,6 +31,7 @@
 template <int RB>
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t ring[1u << RB];
+    uint32_t stream[256];          // compressed words: segment g (64 words) at slot g & 3
     uint32_t lit[1 << LB];
     uint32_t dst[1 << DB];
     uint32_t cl[1 << CB];
@@ -39,50 +43,58 @@ struct __attribute__((aligned(16))) InflateLds {
     uint8_t lens[320];
 };
 
-// v_writelane_b32 (value, lane, old) — the LLVM intrinsic, not exposed as a clang builtin
-extern "C" __device__ int llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane");
-
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 
-// Compressed stream of one chunk: word i (chunk-relative) is base[i].  256 words live across the
-// lanes (lane l holds word wb+l in A and wb+64+l in B), so fetching stream words is v_readlane.
-// A reload is two coalesced dword loads per lane whose results are consumed at once: the wait
-// (~one memory latency per ~500 B of input) is paid there and nowhere else.  A load whose result
-// stayed in flight across loop iterations would make the compiler wait for every outstanding
-// memory operation at each use (including the output flush stores).
+// v_writelane_b32 (value, lane, old) — the LLVM intrinsic, not exposed as a clang builtin
+extern "C" __device__ int llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane");
+
+__device__ __forceinline__ uint32_t bperm(uint32_t byte_addr, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)byte_addr, (int)v);
+}
+
+// Compressed stream of one chunk: word i (chunk-relative) is base[i].  Words move to an LDS ring
+// of four 64-word segments by global_load_lds (straight to LDS, no VGPR in flight).  While the
+// decoder reads segment g, segments g and g+1 are resident and g+2 is loading; entering g+1
+// issues g+3 and waits for everything but that newest load (s_waitcnt vmcnt(1)) — once per
+// 256 B of input.  The compiler does not track LDS-DMA, so every wait is explicit.
 struct Reader {
     const uint32_t *base;
     uint32_t nw;            // readable words from base (>= 1)
-    uint32_t A, B;          // words wb+lane, wb+64+lane
-    uint32_t wb;            // first word of the buffer
+    uint32_t sg;            // segment the decoder is in
     uint32_t wi;            // next word to append to bb
     uint64_t bb;            // bit buffer, LSB = next bit
     uint32_t bn;            // valid bits in bb
 };
 
-__device__ __forceinline__ void rd_load(Reader &r, int lane) {
-    const uint32_t i = r.wb + lane;
-    r.A = i < r.nw ? r.base[i] : 0u;          // past the end: zeros (an overrun is an error anyway)
-    r.B = i + 64 < r.nw ? r.base[i + 64] : 0u;
-    // consume the loads here, so the compiler waits for them in this (rare) block rather than
-    // at every v_readlane of A/B (there the wait would drain every store in flight, too)
-    asm volatile("" ::"v"(r.A), "v"(r.B));
+__device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint32_t g, int lane) {
+    const uint32_t i = min(g * 64 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
+    __builtin_amdgcn_global_load_lds(r.base + i, stream + (g & 3) * 64, 4, 0, 0);
 }
 
-__device__ __forceinline__ uint32_t rd_word(const Reader &r, uint32_t idx) {
-    return idx < 64 ? rdlane(r.A, idx) : rdlane(r.B, idx - 64);
-}
-
-// position the bit buffer at chunk-relative bit `bit` (reloads only when outside the buffer)
-__device__ __forceinline__ void rd_seek(Reader &r, uint32_t bit, int lane) {
-    r.wi = bit >> 5;
-    if (r.wi < r.wb || r.wi >= r.wb + 128) {
-        r.wb = r.wi;
-        rd_load(r, lane);
+// make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
+// runs up to two words ahead of the decode position and may have entered sg already).
+__device__ __forceinline__ void st_enter(Reader &r, uint32_t *stream, uint32_t g, int lane) {
+    if (g == r.sg || g + 1 == r.sg) return;
+    if (g != r.sg + 1) {
+        st_issue(r, stream, g, lane);
+        st_issue(r, stream, g + 1, lane);
     }
-    const uint32_t w = rd_word(r, r.wi - r.wb);
+    st_issue(r, stream, g + 2, lane);
+    r.sg = g;
+    asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t rd_word(Reader &r, uint32_t *stream, uint32_t w, int lane) {
+    st_enter(r, stream, w >> 6, lane);
+    return uni(stream[w & 255]);
+}
+
+// position the bit buffer at chunk-relative bit `bit`
+__device__ __forceinline__ void rd_seek(Reader &r, uint32_t *stream, uint32_t bit, int lane) {
+    r.wi = bit >> 5;
+    const uint32_t w = rd_word(r, stream, r.wi, lane);
     r.wi++;
     const uint32_t sh = bit & 31;
     r.bb = (uint64_t)(w >> sh);
@@ -90,13 +102,9 @@ __device__ __forceinline__ void rd_seek(Reader &r, uint32_t bit, int lane) {
 }
 
 // guarantees bn >= 32
-__device__ __forceinline__ void rd_refill(Reader &r, int lane) {
+__device__ __forceinline__ void rd_refill(Reader &r, uint32_t *stream, int lane) {
     if (r.bn <= 32) {
-        if (r.wi >= r.wb + 128) {
-            r.wb = r.wi;
-            rd_load(r, lane);
-        }
-        const uint32_t w = rd_word(r, r.wi - r.wb);
+        const uint32_t w = rd_word(r, stream, r.wi, lane);
         r.wi++;
         r.bb |= (uint64_t)w << r.bn;
         r.bn += 32;
@@ -104,24 +112,6 @@ __device__ __forceinline__ void rd_refill(Reader &r, int lane) {
 }
 
 __device__ __forceinline__ uint32_t rd_pos(const Reader &r) { return r.wi * 32 - r.bn; }
-
-// Symbol -> entry: the VGPR first level (6 bits), else the LDS root table, else the slow path.
-__device__ __forceinline__ uint32_t lookup(uint32_t vtab, const uint32_t *tab, uint32_t tmask, Reader &r,
-                                           const uint16_t *count, const uint16_t *sorted, int kind) {
-    uint32_t e = rdlane(vtab, (uint32_t)r.bb & 63);
-    if (e == 0) {
-        e = uni(tab[(uint32_t)r.bb & tmask]);
-        if ((e & 15) == 0) e = slow_entry(r, count, sorted, kind);
-    }
-    return e;
-}
-
-// 6-bit first level: the root entry when its code fits 6 bits, else 0 (= go to LDS).
-__device__ __forceinline__ uint32_t first_level(const uint32_t *tab, int lane) {
-    const uint32_t e = tab[lane];
-    const uint32_t L = e & 15;
-    return (L != 0 && L <= 6) ? e : 0u;
-}
 
 // Ring bytes of global output addresses [glo, ghi) -> out; unaligned head/tail singly, the
 // 16-B-aligned middle as ds_read_b128 + global_store_dwordx4 (1 KiB per wave instruction).
@@ -148,8 +138,9 @@ __device__ __forceinline__ void flush_range(const uint8_t *ring, uint8_t *out, u
     }
 }
 
-// Byte at chunk position p older than the ring: the flushed output (p >= 0) or the Point's window.
-// Read as an aligned dword so the compiler never merges it with an LDS byte load into one flat load.
+// Byte at chunk position p older than the ring: the flushed output (p >= 0; this wave's own
+// earlier stores — a wave's accesses to one address are ordered) or the Point's window.  Read as
+// an aligned dword so the compiler never merges it with an LDS byte load into one flat load.
 __device__ __forceinline__ uint32_t far_byte(const uint8_t *out, const uint8_t *dict, uint64_t out_off, int32_t p) {
     const uint8_t *a = p >= 0 ? out + out_off + (uint32_t)p : dict + 32768 + p;   // p >= -32768
     const uint32_t w = *(const uint32_t *)((uintptr_t)a & ~(uintptr_t)3);
@@ -180,9 +171,7 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, co
             }
         }
     } else {
-        // far reference (dist > RING - n >= n): bytes older than the ring come from the flushed
-        // output (this wave's own earlier stores: same-wave accesses to an address are ordered)
-        // or the Point's window
+        // far reference (dist > RING - n >= n)
         for (uint32_t j0 = 0; j0 < n; j0 += 64) {
             const uint32_t j = j0 + lane;
             if (j < n) {
@@ -204,7 +193,10 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                                                          PpgInflateResult *__restrict__ res, int njobs) {
     constexpr uint32_t RING = 1u << RB;
     constexpr uint32_t RM = RING - 1;
-    static_assert(RB >= 13 && RB <= 15, "far back-references assume the ring spans >= 2 flush units");
+    // flush unit: far references (older than the ring) must already be flushed; a round adds at
+    // most 64 + 258 bytes, so UNIT <= RING - 322 keeps them flushed (see copy_match)
+    constexpr uint32_t UNIT = RB >= 13 ? 4096u : RING / 2;
+    static_assert(RB >= 12 && RB <= 15, "ring of 4..32 KiB");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     InflateLds<RB> &S = *reinterpret_cast<InflateLds<RB> *>(smem);
     const int lane = threadIdx.x;
@@ -229,20 +221,23 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     // chunk-relative compressed stream
     const uint64_t w0abs = (J.bit_start >> 5) & ~127ull;
     Reader r;
-    r.wb = 0x80000000u;   // empty buffer: the first seek loads
+    r.sg = 0x7FFFFFF0u;   // nothing resident: the first seek loads
     r.base = comp + w0abs;
     r.nw = (uint32_t)min(nwords > w0abs ? nwords - w0abs : 1ull, 0xFFFFFFFFull);
     const uint32_t bit_limit = (uint32_t)min(J.bit_limit - w0abs * 32, 0xFFFFFFFFull);
-    rd_seek(r, (uint32_t)(J.bit_start - w0abs * 32), lane);
+    rd_seek(r, S.stream, (uint32_t)(J.bit_start - w0abs * 32), lane);
+
+    // lane constants of the round loop
+    const uint64_t lanes_le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // lanes <= this one
+    const uint32_t spec_tok = 0xFFu | ((uint32_t)lane << 8);                  // see vtok below
 
     uint32_t pos = 0;                                        // output bytes produced
     uint32_t fl_done = 0;                                    // flushed up to this position
     uint32_t fl_next = UNIT - (uint32_t)(out_off & (UNIT - 1));   // next global 4 KiB boundary
     int status = ST_OK, flags = 0, last = 0, in_block = 0;
-    uint32_t vlit = 0, vdst = 0;    // first-level tables (one entry per lane)
 
     while (pos < len && !last) {
-        r.wb = uni(r.wb);
+        r.sg = uni(r.sg);
         r.wi = uni(r.wi);
         r.bb = uni64(r.bb);
         r.bn = uni(r.bn);
@@ -250,13 +245,13 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         fl_done = uni(fl_done);
         fl_next = uni(fl_next);
         status = (int)uni((uint32_t)status);
-        rd_refill(r, lane);
+        rd_refill(r, S.stream, lane);
         last = (int)br_take(r, 1);
         const uint32_t type = br_take(r, 2);
         if (type == 0) {
             // ---- stored block ----
             br_take(r, r.bn & 7);
-            rd_refill(r, lane);
+            rd_refill(r, S.stream, lane);
             const uint32_t slen = br_take(r, 16), nlen = br_take(r, 16);
             if ((slen ^ 0xFFFFu) != nlen) { status = ST_DATA_ERROR; break; }
             const uint32_t bytepos = rd_pos(r) >> 3;
@@ -278,7 +273,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                     fl_next += UNIT;
                 }
             }
-            rd_seek(r, (bytepos + copied) * 8, lane);
+            rd_seek(r, S.stream, (bytepos + copied) * 8, lane);
             if (copied < slen) break;   // output full mid-block (zlib stops at avail_out == 0)
             in_block = 0;
             continue;
@@ -298,13 +293,13 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             build_table<DB>(S.lens + 288, 32, S.dst, S.dst_count, S.dst_sorted, TAB_DST, lane);
         } else {
             // ---- dynamic Huffman codes (RFC 1951 3.2.7) ----
-            rd_refill(r, lane);
+            rd_refill(r, S.stream, lane);
             const uint32_t hlit = br_take(r, 5) + 257, hdist = br_take(r, 5) + 1, hclen = br_take(r, 4) + 4;
             if (hlit > 286 || hdist > 30) { status = ST_DATA_ERROR; break; }
             if (lane < 19) S.lens[lane] = 0;
             __syncthreads();
             for (uint32_t i = 0; i < hclen; i++) {
-                rd_refill(r, lane);
+                rd_refill(r, S.stream, lane);
                 const uint32_t v = br_take(r, 3);
                 if (lane == 0) S.lens[c_clorder[i]] = (uint8_t)v;
             }
@@ -314,7 +309,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             const uint32_t total = hlit + hdist;
             bool bad = false;
             while (idx < total) {
-                rd_refill(r, lane);
+                rd_refill(r, S.stream, lane);
                 const uint32_t e = uni(S.cl[(uint32_t)r.bb & ((1u << CB) - 1)]);
                 const uint32_t L = e & 15;
                 if (L == 0) { bad = true; break; }
@@ -339,12 +334,10 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             if (build_table<LB>(S.lens, (int)hlit, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane) != 0) { status = ST_DATA_ERROR; break; }
             if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, S.dst_count, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
         }
-        vlit = first_level(S.lit, lane);
-        vdst = first_level(S.dst, lane);
         in_block = 1;
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
-        // through the outer loop), so the token loop keeps it in SGPRs with scalar branches
-        r.wb = uni(r.wb);
+        // through the outer loop), so the token rounds keep it in SGPRs with scalar branches
+        r.sg = uni(r.sg);
         r.wi = uni(r.wi);
         r.bb = uni64(r.bb);
         r.bn = uni(r.bn);
@@ -353,59 +346,34 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         fl_next = uni(fl_next);
 
         // ---- token rounds ----
-        // Speculative lane-parallel decode: every lane decodes one whole token (litlen code, length
-        // extra bits, distance code, distance extra bits) as if a token started at bit bp + lane.
-        // A scalar walk then follows the real chain of tokens (start, start + bits, ...) through
-        // the lanes, emitting each one, until the chain leaves the 64-bit span; the next round
-        // starts where it left.  Codes longer than the root tables, end-of-block and invalid codes
-        // stop the walk and are decoded by the bit-serial path below.
         uint32_t bp = rd_pos(r);
         while (pos < len) {
-            const uint32_t wq = bp >> 5;
-            if (wq < r.wb || wq + 4 >= r.wb + 128) {
-                r.wb = wq;
-                rd_load(r, lane);
-            }
-            const uint32_t wi = wq - r.wb;
-            uint32_t w0, w1, w2, w3, w4;
-            if (wi + 4 < 64) {
-                w0 = rdlane(r.A, wi); w1 = rdlane(r.A, wi + 1); w2 = rdlane(r.A, wi + 2);
-                w3 = rdlane(r.A, wi + 3); w4 = rdlane(r.A, wi + 4);
-            } else if (wi >= 64) {
-                w0 = rdlane(r.B, wi - 64); w1 = rdlane(r.B, wi - 63); w2 = rdlane(r.B, wi - 62);
-                w3 = rdlane(r.B, wi - 61); w4 = rdlane(r.B, wi - 60);
-            } else {
-                w0 = rd_word(r, wi); w1 = rd_word(r, wi + 1); w2 = rd_word(r, wi + 2);
-                w3 = rd_word(r, wi + 3); w4 = rd_word(r, wi + 4);
-            }
-            // 64 stream bits at bp + lane
-            const uint32_t o = (bp & 31) + (uint32_t)lane;   // 0..94
-            const uint32_t kq = o >> 5, sh = o & 31;
-            const uint32_t x0 = kq == 0 ? w0 : (kq == 1 ? w1 : w2);
-            const uint32_t x1 = kq == 0 ? w1 : (kq == 1 ? w2 : w3);
-            const uint32_t x2 = kq == 0 ? w2 : (kq == 1 ? w3 : w4);
-            const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, sh);
-            const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, sh);
-            // litlen symbol + length extra bits
+            // the 64 stream bits at bp + lane (three words per lane from the LDS stream ring)
+            st_enter(r, S.stream, bp >> 11, lane);
+            const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
+            const uint32_t wl = (bp >> 5) + (o >> 5);
+            const uint32_t x0 = S.stream[wl & 255], x1 = S.stream[(wl + 1) & 255], x2 = S.stream[(wl + 2) & 255];
+            const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, o);      // shift = o & 31
+            const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, o);
+
+            // speculative token at bit bp + lane
             const uint32_t e = S.lit[lo & ((1u << LB) - 1)];
-            const uint32_t L = e & 15, kind = (e >> 4) & 3;
-            const bool islen = kind == K_BASE;
-            const uint64_t xs = ((((uint64_t)hi) << 32) | lo) >> L;
-            const uint32_t xb = islen ? (e >> 8) & 15 : 0u;
-            const uint32_t mlen = (e >> 16) + ((uint32_t)xs & ((1u << xb) - 1));
-            // distance symbol + extra bits (harmless garbage on literal lanes)
-            const uint32_t y = (uint32_t)(xs >> xb);
+            const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
+            const uint32_t xb = (e >> 10) & 31;
+            const uint32_t mlen = (e >> 16) + (r1 & ((1u << xb) - 1));
+            const uint32_t y = r1 >> xb;
             const uint32_t d = S.dst[y & ((1u << DB) - 1)];
-            const uint32_t L2 = d & 15, xd = (d >> 8) & 15;
-            const uint32_t dist = (d >> 16) + ((y >> L2) & ((1u << xd) - 1));
-            const bool special = L == 0 || kind >= K_EOB || (islen && (L2 == 0 || ((d >> 4) & 3) != K_BASE));
-            const uint32_t tb = islen ? L + xb + L2 + xd : L;
+            const uint32_t r2 = y >> (d & 31);                              // past the distance code
+            const uint32_t xd = (d >> 10) & 31;
+            const uint32_t dist = (d >> 16) + (r2 & ((1u << xd) - 1));
+            const bool islen = (e & 0x8000u) != 0;
+            const uint32_t tb = ((e >> 5) & 31) + (islen ? ((d >> 5) & 31) : 0u);
+            const bool special = (e & 15) == 0 || (islen && (d & 15) == 0);
             // token word: [6:0] lane of the next token, [31:23] output bytes; a special token is
             // 0xFF | lane << 8 (next lane 127 ends the walk, 0 bytes)
-            const uint32_t vtok = special ? (0xFFu | ((uint32_t)lane << 8))
-                                          : (((uint32_t)lane + tb) | ((islen ? mlen : 1u) << 23));
+            const uint32_t vtok = special ? spec_tok : (((uint32_t)lane + tb) | ((islen ? mlen : 1u) << 23));
             // token info: [31] match, [15:0] distance (match) or the literal byte
-            const uint32_t vinf = islen ? (0x80000000u | dist) : ((e >> 8) & 255);
+            const uint32_t vinf = islen ? (0x80000000u | dist) : (e >> 16);
 
             // ---- walk the real token chain (wave-uniform): lane s -> lane s + bits(s) ----
             // Records each token's info at the lane of its output offset (vtin) and the offsets in
@@ -430,36 +398,34 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 
             // ---- emit the round's first 64 output bytes, one per lane ----
             {
-                const uint32_t j = (uint32_t)lane;
-                const uint64_t mle = j == 63 ? ~0ull : ((2ull << j) - 1ull);   // lanes <= j
-                const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & mle);   // start of j's token (bit 0 of mo is set)
-                const uint32_t inf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sj << 2), (int)vtin);
-                const bool act = j < rout;
-                const bool ism = (inf >> 31) != 0;
-                const int32_t jj = (int32_t)j - (int32_t)(inf & 0xFFFFu);   // source, relative to the round
-                const bool dep = act && ism && jj >= 0;                      // produced in this round
-                uint32_t val = inf & 255u;
-                if (act && ism && jj < 0 && jj >= -(int32_t)RING) val = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
+                const uint32_t inf = bperm(sj << 2, vtin);
+                const bool ism = (int32_t)inf < 0;
+                const int32_t jj = lane - (int32_t)(inf & 0xFFFFu);   // source, relative to the round
+                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                uint32_t val = ism ? rv : (inf & 255u);
+                const bool act = (uint32_t)lane < rout;
                 const bool far = act && ism && jj < -(int32_t)RING;
                 if (__ballot(far)) {
                     if (far) val = far_byte(out, dict, out_off, (int32_t)pos + jj);
                 }
+                const bool dep = act && ism && jj >= 0;               // produced in this round
                 if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
-                    int32_t ptr = dep ? jj : (int32_t)j;
+                    int32_t ptr = dep ? jj : lane;
                     for (;;) {
-                        const int32_t p2 = __builtin_amdgcn_ds_bpermute(ptr << 2, ptr);
+                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
                         if (!__ballot(p2 != ptr)) break;
                         ptr = p2;
                     }
-                    val = (uint32_t)__builtin_amdgcn_ds_bpermute(ptr << 2, (int)val);
+                    val = bperm((uint32_t)ptr << 2, val);
                 }
-                if (act) S.ring[(rb0 + pos + j) & RM] = (uint8_t)val;
+                if (act) S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
             }
             if (rout > 64) {
                 // the rest of the last token (a match): bytes 64.. of the round
-                const uint32_t last = 63u - (uint32_t)__builtin_clzll(mo);
-                const uint32_t dl = rdlane(vtin, last) & 0xFFFFu;
+                const uint32_t lastt = 63u - (uint32_t)__builtin_clzll(mo);
+                const uint32_t dl = rdlane(vtin, lastt) & 0xFFFFu;
                 copy_match<RB>(S.ring, out, dict, out_off, rb0, pos + 64, dl, rout - 64, lane);
             }
             pos += rout;
@@ -471,32 +437,27 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             bp += s;
             if (!spec) continue;
 
-            // ---- one token by the bit-serial path (long code, end-of-block or error) ----
-            rd_seek(r, bp, lane);
-            rd_refill(r, lane);
-            const uint32_t e1 = lookup(vlit, S.lit, (1u << LB) - 1, r, S.lit_count, S.lit_sorted, TAB_LIT);
-            br_take(r, e1 & 15);
-            const uint32_t kind1 = (e1 >> 4) & 3;
-            if (kind1 == K_LIT) {
-                if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)(e1 >> 8);
+            // ---- one token, bit-serially (long code, end-of-block or invalid) ----
+            rd_seek(r, S.stream, bp, lane);
+            rd_refill(r, S.stream, lane);
+            const int sym = slow_decode(r, S.lit_count, S.lit_sorted);
+            if (sym < 0 || sym >= 286) { status = ST_DATA_ERROR; break; }
+            if (sym < 256) {
+                if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)sym;
                 pos++;
-            } else if (kind1 == K_BASE) {
-                const uint32_t ml = (e1 >> 16) + br_take(r, (e1 >> 8) & 15);
-                rd_refill(r, lane);
-                const uint32_t d1 = lookup(vdst, S.dst, (1u << DB) - 1, r, S.dst_count, S.dst_sorted, TAB_DST);
-                br_take(r, d1 & 15);
-                if (((d1 >> 4) & 3) != K_BASE) { status = ST_DATA_ERROR; break; }
-                const uint32_t ds = (d1 >> 16) + br_take(r, (d1 >> 8) & 15);
-                const uint32_t n = min(ml, len - pos);
-                copy_match<RB>(S.ring, out, dict, out_off, rb0, pos, ds, n, lane);
-                pos += n;
-            } else if (kind1 == K_EOB) {
+            } else if (sym == 256) {
                 in_block = 0;
                 bp = rd_pos(r);
                 break;
             } else {
-                status = ST_DATA_ERROR;
-                break;
+                const uint32_t ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
+                rd_refill(r, S.stream, lane);
+                const int dsym = slow_decode(r, S.dst_count, S.dst_sorted);
+                if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
+                const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
+                const uint32_t n = min(ml, len - pos);
+                copy_match<RB>(S.ring, out, dict, out_off, rb0, pos, ds, n, lane);
+                pos += n;
             }
             bp = rd_pos(r);
             if (pos >= fl_next) {
@@ -505,8 +466,8 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 fl_next += UNIT;
             }
         }
-        if (status == ST_OK) rd_seek(r, bp, lane);   // the next block header / the R-E5 check read from bp
         if (status != ST_OK) break;
+        rd_seek(r, S.stream, bp, lane);   // the next block header / the R-E5 check read from bp
     }
     flush_range<RB>(S.ring, out, out_off + fl_done, out_off + pos, lane);
 
@@ -518,14 +479,9 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         if (status == ST_OK) status = ST_DATA_ERROR;
     }
     if (status == ST_OK && in_block && pos == len) {
-        rd_refill(r, lane);
-        const uint32_t e = lookup(vlit, S.lit, (1u << LB) - 1, r, S.lit_count, S.lit_sorted, TAB_LIT);
-        if (((e >> 4) & 3) == K_EOB) {
-            br_take(r, e & 15);
-            end_bit = rd_pos(r);
-        } else {
-            flags |= PPG_FLAG_NO_EOB;
-        }
+        rd_refill(r, S.stream, lane);
+        if (slow_decode(r, S.lit_count, S.lit_sorted) == 256) end_bit = rd_pos(r);
+        else flags |= PPG_FLAG_NO_EOB;
     }
     if (lane == 0) {
         res[k].produced = pos;
@@ -540,6 +496,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 // ------------------------------------------------------------------------------------------
 size_t ppg_inflate_lds_bytes(int ring_bits) {
     switch (ring_bits) {
+        case 12: return sizeof(InflateLds<12>);
         case 13: return sizeof(InflateLds<13>);
         case 14: return sizeof(InflateLds<14>);
         default: return sizeof(InflateLds<15>);
@@ -551,6 +508,10 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, const uint32_t *comp
                               int njobs) {
     if (njobs <= 0) return hipSuccess;
     switch (ring_bits) {
+        case 12:
+            hipLaunchKernelGGL(ppg_inflate_kernel<12>, dim3(njobs), dim3(64), sizeof(InflateLds<12>), s, comp, nwords,
+                               jobs, dicts, out, res, njobs);
+            break;
         case 13:
             hipLaunchKernelGGL(ppg_inflate_kernel<13>, dim3(njobs), dim3(64), sizeof(InflateLds<13>), s, comp, nwords,
                                jobs, dicts, out, res, njobs);
