@@ -333,7 +333,7 @@ const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    int ring_bits = 12;   // inflate history ring: 2^12..2^15 bytes of LDS per wavefront (4 KiB: 16 waves/CU)
+    int ring_bits = 11;   // inflate history ring: 2^11..2^15 bytes of LDS per wavefront (2 KiB: 24 waves/CU)
 };
 
 namespace {
@@ -381,7 +381,7 @@ int ppg_open(int device, ppg_ctx **out) {
     auto ctx = std::make_unique<ppg_ctx>();
     ctx->device = device;
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(12, atoi(rb)));
+    if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(11, atoi(rb)));
     *out = ctx.release();
     return PPG_OK;
 }

@@ -32,6 +32,10 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
 }
 
+__device__ __forceinline__ uint32_t rdlane_u(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
 __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int kind) {
     if (kind == TAB_CL) return len | (sym << 8);
     if (kind == TAB_LIT) {
@@ -53,20 +57,27 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int k
 template <int TB>
 __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t *count_lds, uint16_t *sorted,
                            int kind, int lane) {
-    uint32_t cnt[16];
-#pragma unroll
-    for (int l = 0; l < 16; l++) cnt[l] = 0;
+    // Runs once per block, so it is written for few registers, not speed: per-length counts,
+    // offsets and running ranks live one per lane (lane l holds length l), loops stay rolled.
+    uint32_t cnt = 0;
     for (int g = 0; g < n; g += 64) {
-        int s = g + lane;
-        uint32_t L = s < n ? lens[s] : 0u;
-#pragma unroll
-        for (int l = 1; l < 16; l++) cnt[l] += (uint32_t)__popcll(__ballot(L == (uint32_t)l));
+        const int s = g + lane;
+        const uint32_t L = s < n ? lens[s] : 0u;
+#pragma unroll 1
+        for (uint32_t l = 1; l < 16; l++) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(L == l));
+            if ((uint32_t)lane == l) cnt += c;
+        }
     }
     int left = 1, maxl = 0;
-#pragma unroll
-    for (int l = 1; l < 16; l++) {
-        left = left * 2 - (int)cnt[l];
-        if (cnt[l]) maxl = l;
+    uint32_t offs = 0, run = 0;
+#pragma unroll 1
+    for (uint32_t l = 1; l < 16; l++) {
+        const uint32_t c = rdlane_u(cnt, l);
+        left = left * 2 - (int)c;       // stays negative once over-subscribed
+        if (c) maxl = (int)l;
+        if ((uint32_t)lane == l) offs = run;
+        run += c;
     }
     if (maxl != 0) {
         if (left < 0) return -1;
@@ -74,41 +85,33 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t
     } else if (kind == TAB_CL) {
         return -1;  // zlib accepts the empty set, then fails with "missing end-of-block"
     }
-    uint32_t offs[16], seen[16];
-    offs[0] = 0;
-    offs[1] = 0;
-#pragma unroll
-    for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + cnt[l];
-#pragma unroll
-    for (int l = 0; l < 16; l++) seen[l] = 0;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t seen = 0;
     for (int g = 0; g < n; g += 64) {
-        int s = g + lane;
-        uint32_t L = s < n ? lens[s] : 0u;
+        const int s = g + lane;
+        const uint32_t L = s < n ? lens[s] : 0u;
         uint32_t mypos = 0;
-#pragma unroll
-        for (int l = 1; l < 16; l++) {
-            uint64_t m = __ballot(L == (uint32_t)l);
-            if (L == (uint32_t)l) mypos = offs[l] + seen[l] + (uint32_t)__popcll(m & lt);
-            seen[l] += (uint32_t)__popcll(m);
+#pragma unroll 1
+        for (uint32_t l = 1; l < 16; l++) {
+            const uint64_t m = __ballot(L == l);
+            if (m) {
+                const uint32_t base = rdlane_u(offs, l) + rdlane_u(seen, l);
+                if (L == l) mypos = base + (uint32_t)__popcll(m & lt);
+                if ((uint32_t)lane == l) seen += (uint32_t)__popcll(m);
+            }
         }
         if (L) sorted[mypos] = (uint16_t)s;
     }
-    if (count_lds) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int l = 0; l < 16; l++) c = (lane == l) ? cnt[l] : c;
-        if (lane < 16) count_lds[lane] = (uint16_t)c;
-    }
+    if (count_lds && lane < 16) count_lds[lane] = (uint16_t)(lane == 0 ? 0u : cnt);
     __syncthreads();
     for (int e0 = 0; e0 < (1 << TB); e0 += 64) {   // uniform trip count (see ppg_inflate_kernel)
         const int e = e0 + lane;
         uint32_t code = 0, first = 0, index = 0, entry = 0;
         bool found = false;
-#pragma unroll
+#pragma unroll 1
         for (int l = 1; l <= TB; l++) {
             code |= ((uint32_t)e >> (l - 1)) & 1u;
-            uint32_t c = cnt[l];
+            const uint32_t c = rdlane_u(cnt, (uint32_t)l);
             if (!found && code - first < c) {
                 entry = make_entry(sorted[index + code - first], (uint32_t)l, kind);
                 found = true;

@@ -31,13 +31,17 @@
 template <int RB>
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t ring[1u << RB];
-    uint32_t stream[256];          // compressed words: segment g (64 words) at slot g & 3
-    uint32_t lit[1 << LB];
+    uint32_t stream[128];          // compressed words: segment g (32 words) at slot g & 3
+    union {                        // the code-length code is dead once the litlen table is built
+        uint32_t lit[1 << LB];
+        uint32_t cl[1 << CB];
+    };
     uint32_t dst[1 << DB];
-    uint32_t cl[1 << CB];
-    uint16_t lit_sorted[288];
+    union {
+        uint16_t lit_sorted[288];
+        uint16_t cl_sorted[20];
+    };
     uint16_t dst_sorted[32];
-    uint16_t cl_sorted[20];
     uint16_t lit_count[16];
     uint16_t dst_count[16];
     uint8_t lens[320];
@@ -55,10 +59,10 @@ __device__ __forceinline__ uint32_t bperm(uint32_t byte_addr, uint32_t v) {
 }
 
 // Compressed stream of one chunk: word i (chunk-relative) is base[i].  Words move to an LDS ring
-// of four 64-word segments by global_load_lds (straight to LDS, no VGPR in flight).  While the
+// of four 32-word segments by global_load_lds (straight to LDS, no VGPR in flight).  While the
 // decoder reads segment g, segments g and g+1 are resident and g+2 is loading; entering g+1
 // issues g+3 and waits for everything but that newest load (s_waitcnt vmcnt(1)) — once per
-// 256 B of input.  The compiler does not track LDS-DMA, so every wait is explicit.
+// 128 B of input.  The compiler does not track LDS-DMA, so every wait is explicit.
 struct Reader {
     const uint32_t *base;
     uint32_t nw;            // readable words from base (>= 1)
@@ -69,8 +73,8 @@ struct Reader {
 };
 
 __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint32_t g, int lane) {
-    const uint32_t i = min(g * 64 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
-    __builtin_amdgcn_global_load_lds(r.base + i, stream + (g & 3) * 64, 4, 0, 0);
+    const uint32_t i = min(g * 32 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
+    if (lane < 32) __builtin_amdgcn_global_load_lds(r.base + i, stream + (g & 3) * 32, 4, 0, 0);
 }
 
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
@@ -87,8 +91,8 @@ __device__ __forceinline__ void st_enter(Reader &r, uint32_t *stream, uint32_t g
 }
 
 __device__ __forceinline__ uint32_t rd_word(Reader &r, uint32_t *stream, uint32_t w, int lane) {
-    st_enter(r, stream, w >> 6, lane);
-    return uni(stream[w & 255]);
+    st_enter(r, stream, w >> 5, lane);
+    return uni(stream[w & 127]);
 }
 
 // position the bit buffer at chunk-relative bit `bit`
@@ -151,10 +155,10 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *out, const uint8_t *
 template <int RB>
 __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, const uint8_t *dict, uint64_t out_off,
                                            uint32_t rb0, uint32_t pos, uint32_t dist, uint32_t n, int lane) {
-    constexpr uint32_t RING = 1u << RB;
-    constexpr uint32_t RM = RING - 1;
+    constexpr uint32_t RM = (1u << RB) - 1;
+    constexpr uint32_t REACH = (1u << RB) - 64;   // ring bytes a reference may use (see the emit)
     const uint32_t dst0 = rb0 + pos;   // ring slot of the first output byte
-    if (dist + n <= RING) {
+    if (dist + n <= REACH) {
         // source entirely in the ring and never overwritten by this copy; every source byte
         // precedes pos, so no 64-byte group reads another group's output
         const uint32_t src0 = dst0 - dist;
@@ -171,14 +175,14 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, co
             }
         }
     } else {
-        // far reference (dist > RING - n >= n)
+        // far reference (dist > REACH - n >= n)
         for (uint32_t j0 = 0; j0 < n; j0 += 64) {
             const uint32_t j = j0 + lane;
             if (j < n) {
                 const uint32_t back = dist - j;                 // source = pos - back
                 const int32_t rel = (int32_t)pos - (int32_t)back;
                 uint32_t v;
-                if (back + n <= RING) v = ring[(dst0 - back) & RM];
+                if (back + n <= REACH) v = ring[(dst0 - back) & RM];
                 else v = far_byte(out, dict, out_off, rel);
                 ring[(dst0 + j) & RM] = (uint8_t)v;
             }
@@ -193,10 +197,10 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                                                          PpgInflateResult *__restrict__ res, int njobs) {
     constexpr uint32_t RING = 1u << RB;
     constexpr uint32_t RM = RING - 1;
-    // flush unit: far references (older than the ring) must already be flushed; a round adds at
-    // most 64 + 258 bytes, so UNIT <= RING - 322 keeps them flushed (see copy_match)
+    // flush unit: far references (older than REACH = RING - 64) must already be flushed; a round
+    // adds at most 64 + 258 bytes, so UNIT <= RING - 386 keeps them flushed (see copy_match)
     constexpr uint32_t UNIT = RB >= 13 ? 4096u : RING / 2;
-    static_assert(RB >= 12 && RB <= 15, "ring of 4..32 KiB");
+    static_assert(RB >= 11 && RB <= 15, "ring of 2..32 KiB");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     InflateLds<RB> &S = *reinterpret_cast<InflateLds<RB> *>(smem);
     const int lane = threadIdx.x;
@@ -349,10 +353,10 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         uint32_t bp = rd_pos(r);
         while (pos < len) {
             // the 64 stream bits at bp + lane (three words per lane from the LDS stream ring)
-            st_enter(r, S.stream, bp >> 11, lane);
+            st_enter(r, S.stream, bp >> 10, lane);
             const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
             const uint32_t wl = (bp >> 5) + (o >> 5);
-            const uint32_t x0 = S.stream[wl & 255], x1 = S.stream[(wl + 1) & 255], x2 = S.stream[(wl + 2) & 255];
+            const uint32_t x0 = S.stream[wl & 127], x1 = S.stream[(wl + 1) & 127], x2 = S.stream[(wl + 2) & 127];
             const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, o);      // shift = o & 31
             const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, o);
 
@@ -366,50 +370,61 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             const uint32_t r2 = y >> (d & 31);                              // past the distance code
             const uint32_t xd = (d >> 10) & 31;
             const uint32_t dist = (d >> 16) + (r2 & ((1u << xd) - 1));
-            const bool islen = (e & 0x8000u) != 0;
-            const uint32_t tb = ((e >> 5) & 31) + (islen ? ((d >> 5) & 31) : 0u);
-            const bool special = (e & 15) == 0 || (islen && (d & 15) == 0);
+            const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);          // length symbol: all ones
+            const uint32_t tb = ((e >> 5) & 31) + (((d >> 5) & 31) & lm);
+            const uint32_t nb = ((mlen - 1) & lm) + 1;                          // output bytes
+            // special: litlen code not in the root table (EOB / invalid / long), or a length whose
+            // distance code is not
+            const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
             // token word: [6:0] lane of the next token, [31:23] output bytes; a special token is
             // 0xFF | lane << 8 (next lane 127 ends the walk, 0 bytes)
-            const uint32_t vtok = special ? spec_tok : (((uint32_t)lane + tb) | ((islen ? mlen : 1u) << 23));
-            // token info: [31] match, [15:0] distance (match) or the literal byte
-            const uint32_t vinf = islen ? (0x80000000u | dist) : (e >> 16);
+            const uint32_t vtok = ((((uint32_t)lane + tb) | (nb << 23)) & ~sm) | (spec_tok & sm);
+            // token info (never 0): [31] match, [15:0] distance; literal: 0x400 | byte, so that
+            // lane - info[15:0] is negative and never "far" for literals (see the emit)
+            const uint32_t vinf = ((0x80000000u | dist) & lm) | ((0x400u | (e >> 16)) & ~lm);
 
             // ---- walk the real token chain (wave-uniform): lane s -> lane s + bits(s) ----
-            // Records each token's info at the lane of its output offset (vtin) and the offsets in
-            // the mask mo; stops when the chain leaves the 64-bit span, at a special token (which
-            // is recorded with 0 bytes, harmlessly), or once no further token can start inside
-            // the first lim output bytes of the round.
-            const uint32_t lim = min(64u, len - pos);
-            const uint32_t cl = 64u - lim;   // off < lim  <=>  off + cl < 64
+            // Each token's info goes to the lane of its output offset (vtin); the walk stops when
+            // the chain leaves the 64-bit span, at a special token (recorded with 0 bytes,
+            // harmlessly), or once no further token can start inside the round's first
+            // min(64, len - pos) output bytes.
             uint32_t s = 0, off = 0, t;
-            uint64_t mo = 0;
             uint32_t vtin = 0;
-            do {
-                t = rdlane(vtok, s);
-                mo |= 1ull << off;
-                vtin = (uint32_t)llvm_writelane((int)rdlane(vinf, s), (int)off, (int)vtin);
-                off += t >> 23;
-                s = t & 127u;
-            } while (max(s, off + cl) < 64u);
+            if (len - pos >= 64) {
+                do {
+                    t = rdlane(vtok, s);
+                    vtin = (uint32_t)llvm_writelane((int)rdlane(vinf, s), (int)off, (int)vtin);
+                    off += t >> 23;
+                    s = t & 127u;
+                } while ((s | off) < 64u);
+            } else {
+                const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
+                do {
+                    t = rdlane(vtok, s);
+                    vtin = (uint32_t)llvm_writelane((int)rdlane(vinf, s), (int)off, (int)vtin);
+                    off += t >> 23;
+                    s = t & 127u;
+                } while (max(s, off + cl) < 64u);
+            }
             const bool spec = (t & 0x80u) != 0;
             if (spec) s = (t >> 8) & 63u;
             const uint32_t rout = min(off, len - pos);   // output bytes of this round
 
             // ---- emit the round's first 64 output bytes, one per lane ----
+            // All 64 lanes write: lanes past rout leave garbage in the slots of positions
+            // [pos + rout, pos + 64), which later rounds overwrite before use; the slots' previous
+            // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
+            // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
             {
+                const uint64_t mo = __ballot(vtin != 0);                              // token offsets
                 const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
                 const uint32_t inf = bperm(sj << 2, vtin);
-                const bool ism = (int32_t)inf < 0;
                 const int32_t jj = lane - (int32_t)(inf & 0xFFFFu);   // source, relative to the round
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val = ism ? rv : (inf & 255u);
-                const bool act = (uint32_t)lane < rout;
-                const bool far = act && ism && jj < -(int32_t)RING;
-                if (__ballot(far)) {
-                    if (far) val = far_byte(out, dict, out_off, (int32_t)pos + jj);
-                }
-                const bool dep = act && ism && jj >= 0;               // produced in this round
+                uint32_t val = (int32_t)inf < 0 ? rv : (inf & 255u);
+                if (jj < -(int32_t)(RING - 64))                       // far (literals: jj > -1280)
+                    val = far_byte(out, dict, out_off, (int32_t)pos + jj);
+                const bool dep = jj >= 0;                             // produced in this round
                 if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
                     int32_t ptr = dep ? jj : lane;
@@ -420,11 +435,11 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                     }
                     val = bperm((uint32_t)ptr << 2, val);
                 }
-                if (act) S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
+                S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
             }
             if (rout > 64) {
                 // the rest of the last token (a match): bytes 64.. of the round
-                const uint32_t lastt = 63u - (uint32_t)__builtin_clzll(mo);
+                const uint32_t lastt = 63u - (uint32_t)__builtin_clzll(__ballot(vtin != 0));
                 const uint32_t dl = rdlane(vtin, lastt) & 0xFFFFu;
                 copy_match<RB>(S.ring, out, dict, out_off, rb0, pos + 64, dl, rout - 64, lane);
             }
@@ -496,6 +511,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 // ------------------------------------------------------------------------------------------
 size_t ppg_inflate_lds_bytes(int ring_bits) {
     switch (ring_bits) {
+        case 11: return sizeof(InflateLds<11>);
         case 12: return sizeof(InflateLds<12>);
         case 13: return sizeof(InflateLds<13>);
         case 14: return sizeof(InflateLds<14>);
@@ -508,6 +524,10 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, const uint32_t *comp
                               int njobs) {
     if (njobs <= 0) return hipSuccess;
     switch (ring_bits) {
+        case 11:
+            hipLaunchKernelGGL(ppg_inflate_kernel<11>, dim3(njobs), dim3(64), sizeof(InflateLds<11>), s, comp, nwords,
+                               jobs, dicts, out, res, njobs);
+            break;
         case 12:
             hipLaunchKernelGGL(ppg_inflate_kernel<12>, dim3(njobs), dim3(64), sizeof(InflateLds<12>), s, comp, nwords,
                                jobs, dicts, out, res, njobs);
