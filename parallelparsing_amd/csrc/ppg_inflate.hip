@@ -31,7 +31,7 @@
 template <int RB>
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t ring[1u << RB];
-    uint32_t stream[128];          // compressed words: segment g (32 words) at slot g & 3
+    uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,130) mirror [0,2)
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LB];
         uint32_t cl[1 << CB];
@@ -75,6 +75,8 @@ struct Reader {
 __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint32_t g, int lane) {
     const uint32_t i = min(g * 32 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
     if (lane < 32) __builtin_amdgcn_global_load_lds(r.base + i, stream + (g & 3) * 32, 4, 0, 0);
+    // slot 0's first words again after slot 3, so a lane's three consecutive words never wrap
+    if ((g & 3) == 0 && lane < 2) __builtin_amdgcn_global_load_lds(r.base + i, stream + 128, 4, 0, 0);
 }
 
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 
     // lane constants of the round loop
     const uint64_t lanes_le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // lanes <= this one
-    const uint32_t spec_tok = 0xFFu | ((uint32_t)lane << 8);                  // see vtok below
+    const uint32_t spec_tok = 127u | ((0x400u | (uint32_t)lane) << 17);       // see vtok below
 
     uint32_t pos = 0;                                        // output bytes produced
     uint32_t fl_done = 0;                                    // flushed up to this position
@@ -355,8 +357,8 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             // the 64 stream bits at bp + lane (three words per lane from the LDS stream ring)
             st_enter(r, S.stream, bp >> 10, lane);
             const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
-            const uint32_t wl = (bp >> 5) + (o >> 5);
-            const uint32_t x0 = S.stream[wl & 127], x1 = S.stream[(wl + 1) & 127], x2 = S.stream[(wl + 2) & 127];
+            const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
+            const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2];
             const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, o);      // shift = o & 31
             const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, o);
 
@@ -376,12 +378,13 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             // special: litlen code not in the root table (EOB / invalid / long), or a length whose
             // distance code is not
             const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
-            // token word: [6:0] lane of the next token, [31:23] output bytes; a special token is
-            // 0xFF | lane << 8 (next lane 127 ends the walk, 0 bytes)
-            const uint32_t vtok = ((((uint32_t)lane + tb) | (nb << 23)) & ~sm) | (spec_tok & sm);
-            // token info (never 0): [31] match, [15:0] distance; literal: 0x400 | byte, so that
-            // lane - info[15:0] is negative and never "far" for literals (see the emit)
-            const uint32_t vinf = ((0x80000000u | dist) & lm) | ((0x400u | (e >> 16)) & ~lm);
+            // token word: [6:0] lane of the next token, [15:7] output bytes, [16] match,
+            // [31:17] distance - 1 (match) or 0x400 | byte (literal: lane - 1 - field is then
+            // negative and never "far", see the emit).  A special token is 127 | (0x400 | lane) << 17:
+            // next lane 127 ends the walk, 0 bytes.  Never 0 (the emit finds tokens by that).
+            const uint32_t field = ((dist - 1) & lm) | ((0x400u | (e >> 16)) & ~lm);
+            const uint32_t vtok = ((((uint32_t)lane + tb) | (nb << 7) | (lm & 0x10000u) | (field << 17)) & ~sm) |
+                                  (spec_tok & sm);
 
             // ---- walk the real token chain (wave-uniform): lane s -> lane s + bits(s) ----
             // Each token's info goes to the lane of its output offset (vtin); the walk stops when
@@ -393,21 +396,21 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             if (len - pos >= 64) {
                 do {
                     t = rdlane(vtok, s);
-                    vtin = (uint32_t)llvm_writelane((int)rdlane(vinf, s), (int)off, (int)vtin);
-                    off += t >> 23;
+                    vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
+                    off += (t >> 7) & 511u;
                     s = t & 127u;
                 } while ((s | off) < 64u);
             } else {
                 const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
                 do {
                     t = rdlane(vtok, s);
-                    vtin = (uint32_t)llvm_writelane((int)rdlane(vinf, s), (int)off, (int)vtin);
-                    off += t >> 23;
+                    vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
+                    off += (t >> 7) & 511u;
                     s = t & 127u;
                 } while (max(s, off + cl) < 64u);
             }
-            const bool spec = (t & 0x80u) != 0;
-            if (spec) s = (t >> 8) & 63u;
+            const bool spec = s == 127u;
+            if (spec) s = (t >> 17) & 63u;
             const uint32_t rout = min(off, len - pos);   // output bytes of this round
 
             // ---- emit the round's first 64 output bytes, one per lane ----
@@ -419,9 +422,9 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 const uint64_t mo = __ballot(vtin != 0);                              // token offsets
                 const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
                 const uint32_t inf = bperm(sj << 2, vtin);
-                const int32_t jj = lane - (int32_t)(inf & 0xFFFFu);   // source, relative to the round
+                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val = (int32_t)inf < 0 ? rv : (inf & 255u);
+                uint32_t val = (inf & 0x10000u) ? rv : ((inf >> 17) & 255u);
                 if (jj < -(int32_t)(RING - 64))                       // far (literals: jj > -1280)
                     val = far_byte(out, dict, out_off, (int32_t)pos + jj);
                 const bool dep = jj >= 0;                             // produced in this round
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             if (rout > 64) {
                 // the rest of the last token (a match): bytes 64.. of the round
                 const uint32_t lastt = 63u - (uint32_t)__builtin_clzll(__ballot(vtin != 0));
-                const uint32_t dl = rdlane(vtin, lastt) & 0xFFFFu;
+                const uint32_t dl = (rdlane(vtin, lastt) >> 17) + 1;
                 copy_match<RB>(S.ring, out, dict, out_off, rb0, pos + 64, dl, rout - 64, lane);
             }
             pos += rout;
