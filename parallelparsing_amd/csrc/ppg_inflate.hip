@@ -31,7 +31,7 @@
 template <int RB>
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t ring[1u << RB];
-    uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,130) mirror [0,2)
+    uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LB];
         uint32_t cl[1 << CB];
@@ -76,7 +76,7 @@ __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint
     const uint32_t i = min(g * 32 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
     if (lane < 32) __builtin_amdgcn_global_load_lds(r.base + i, stream + (g & 3) * 32, 4, 0, 0);
     // slot 0's first words again after slot 3, so a lane's three consecutive words never wrap
-    if ((g & 3) == 0 && lane < 2) __builtin_amdgcn_global_load_lds(r.base + i, stream + 128, 4, 0, 0);
+    if ((g & 3) == 0 && lane < 4) __builtin_amdgcn_global_load_lds(r.base + i, stream + 128, 4, 0, 0);
 }
 
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
@@ -192,6 +192,33 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, co
     }
 }
 
+// One speculative token from the 64 stream bits (lo, hi) at some bit offset, decoded with the
+// root tables.  Token word: [7:0] index of the next token's bit offset (this lane + its bits),
+// [16:8] output bytes (1: literal), [31:17] distance - 1 (match) or 0x400 | byte (literal: then
+// lane - 1 - field is negative and never "far", see the emit).  A special token (a code the
+// root tables do not resolve: end-of-block, invalid, long) is 255 | (0x400 | lane) << 17: next
+// index 255 ends the walk, 0 bytes.  Never 0 (the emit finds tokens by that).
+__device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32_t *dst, uint32_t lo, uint32_t hi,
+                                               uint32_t lane) {
+    const uint32_t e = lit[lo & ((1u << LB) - 1)];
+    const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
+    const uint32_t xb = (e >> 10) & 31;
+    const uint32_t mlen = (e >> 16) + (r1 & ((1u << xb) - 1));
+    const uint32_t y = r1 >> xb;
+    const uint32_t d = dst[y & ((1u << DB) - 1)];
+    const uint32_t r2 = y >> (d & 31);                              // past the distance code
+    const uint32_t xd = (d >> 10) & 31;
+    const uint32_t dist = (d >> 16) + (r2 & ((1u << xd) - 1));
+    const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);       // length symbol: all ones
+    const uint32_t tb = ((e >> 5) & 31) + (((d >> 5) & 31) & lm);
+    const uint32_t nb = ((mlen - 1) & lm) + 1;                      // output bytes
+    const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
+    const uint32_t field = ((dist - 1) & lm) | ((0x400u | (e >> 16)) & ~lm);
+    const uint32_t tok = (lane + tb) | (nb << 8) | (field << 17);
+    const uint32_t spec = 255u | ((0x400u | lane) << 17);
+    return (tok & ~sm) | (spec & sm);
+}
+
 template <int RB>
 __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
@@ -235,7 +262,6 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 
     // lane constants of the round loop
     const uint64_t lanes_le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);   // lanes <= this one
-    const uint32_t spec_tok = 127u | ((0x400u | (uint32_t)lane) << 17);       // see vtok below
 
     uint32_t pos = 0;                                        // output bytes produced
     uint32_t fl_done = 0;                                    // flushed up to this position
@@ -354,63 +380,62 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         // ---- token rounds ----
         uint32_t bp = rd_pos(r);
         while (pos < len) {
-            // the 64 stream bits at bp + lane (three words per lane from the LDS stream ring)
+            // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS ring)
             st_enter(r, S.stream, bp >> 10, lane);
             const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
             const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
-            const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2];
-            const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, o);      // shift = o & 31
-            const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, o);
+            const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2], x3 = sw[3], x4 = sw[4];
+            // speculative tokens at every bit offset of the 128-bit span (two per lane)
+            const uint32_t vta = spec_token(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
+                                            __builtin_amdgcn_alignbit(x2, x1, o), (uint32_t)lane);
+            const uint32_t vtb = spec_token(S.lit, S.dst, __builtin_amdgcn_alignbit(x3, x2, o),
+                                            __builtin_amdgcn_alignbit(x4, x3, o), (uint32_t)lane);
 
-            // speculative token at bit bp + lane
-            const uint32_t e = S.lit[lo & ((1u << LB) - 1)];
-            const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
-            const uint32_t xb = (e >> 10) & 31;
-            const uint32_t mlen = (e >> 16) + (r1 & ((1u << xb) - 1));
-            const uint32_t y = r1 >> xb;
-            const uint32_t d = S.dst[y & ((1u << DB) - 1)];
-            const uint32_t r2 = y >> (d & 31);                              // past the distance code
-            const uint32_t xd = (d >> 10) & 31;
-            const uint32_t dist = (d >> 16) + (r2 & ((1u << xd) - 1));
-            const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);          // length symbol: all ones
-            const uint32_t tb = ((e >> 5) & 31) + (((d >> 5) & 31) & lm);
-            const uint32_t nb = ((mlen - 1) & lm) + 1;                          // output bytes
-            // special: litlen code not in the root table (EOB / invalid / long), or a length whose
-            // distance code is not
-            const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
-            // token word: [6:0] lane of the next token, [15:7] output bytes, [16] match,
-            // [31:17] distance - 1 (match) or 0x400 | byte (literal: lane - 1 - field is then
-            // negative and never "far", see the emit).  A special token is 127 | (0x400 | lane) << 17:
-            // next lane 127 ends the walk, 0 bytes.  Never 0 (the emit finds tokens by that).
-            const uint32_t field = ((dist - 1) & lm) | ((0x400u | (e >> 16)) & ~lm);
-            const uint32_t vtok = ((((uint32_t)lane + tb) | (nb << 7) | (lm & 0x10000u) | (field << 17)) & ~sm) |
-                                  (spec_tok & sm);
-
-            // ---- walk the real token chain (wave-uniform): lane s -> lane s + bits(s) ----
-            // Each token's info goes to the lane of its output offset (vtin); the walk stops when
-            // the chain leaves the 64-bit span, at a special token (recorded with 0 bytes,
-            // harmlessly), or once no further token can start inside the round's first
-            // min(64, len - pos) output bytes.
-            uint32_t s = 0, off = 0, t;
+            // ---- walk the real token chain (wave-uniform): offset s -> s + bits(s) ----
+            // Each token goes to the lane of its output offset (vtin).  The walk runs through the
+            // first 64 offsets (vta), then the next 64 (vtb), and stops at a special token
+            // (recorded with 0 bytes, harmlessly), past the span, or once no further token can
+            // start inside the round's first min(64, len - pos) output bytes.
+            uint32_t s = 0, off = 0, t = 0, half = 0;
             uint32_t vtin = 0;
             if (len - pos >= 64) {
                 do {
-                    t = rdlane(vtok, s);
+                    t = rdlane(vta, s);
                     vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                    off += (t >> 7) & 511u;
-                    s = t & 127u;
+                    off += (t >> 8) & 511u;
+                    s = t & 255u;
                 } while ((s | off) < 64u);
+                if (off < 64 && s != 255u) {   // crossed into the second 64 offsets
+                    s -= 64;
+                    half = 64;
+                    do {
+                        t = rdlane(vtb, s);
+                        vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
+                        off += (t >> 8) & 511u;
+                        s = t & 255u;
+                    } while ((s | off) < 64u);
+                }
             } else {
                 const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
                 do {
-                    t = rdlane(vtok, s);
+                    t = rdlane(vta, s);
                     vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                    off += (t >> 7) & 511u;
-                    s = t & 127u;
+                    off += (t >> 8) & 511u;
+                    s = t & 255u;
                 } while (max(s, off + cl) < 64u);
+                if (off + cl < 64 && s != 255u) {
+                    s -= 64;
+                    half = 64;
+                    do {
+                        t = rdlane(vtb, s);
+                        vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
+                        off += (t >> 8) & 511u;
+                        s = t & 255u;
+                    } while (max(s, off + cl) < 64u);
+                }
             }
-            const bool spec = s == 127u;
-            if (spec) s = (t >> 17) & 63u;
+            const bool spec = s == 255u;
+            s = half + (spec ? ((t >> 17) & 63u) : s);   // bit offset of the next token
             const uint32_t rout = min(off, len - pos);   // output bytes of this round
 
             // ---- emit the round's first 64 output bytes, one per lane ----
@@ -424,7 +449,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 const uint32_t inf = bperm(sj << 2, vtin);
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val = (inf & 0x10000u) ? rv : ((inf >> 17) & 255u);
+                uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 if (jj < -(int32_t)(RING - 64))                       // far (literals: jj > -1280)
                     val = far_byte(out, dict, out_off, (int32_t)pos + jj);
                 const bool dep = jj >= 0;                             // produced in this round
