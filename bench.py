@@ -50,7 +50,7 @@ def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
     """The oracle's threaded DecompressAll (C restatement of BatchedFASTQ over zlib 1.2.11) on a
     bounded prefix of the same file, timed on this host (rank 0, N = 1 only)."""
     from oracle import oracle as O
-    sample = min(nchunks, int(os.environ.get("PPG_CPU_SAMPLE_CHUNKS", "2048")))
+    sample = min(nchunks, int(os.environ.get("PPG_CPU_SAMPLE_CHUNKS", "4096")))
     hi = int(ix_in[sample])
     gz = tf.file_bytes(0, hi)
     win, offs = tf.windows(0, sample + 1)
@@ -67,6 +67,20 @@ def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
             "decompressed_MBps": out_bytes / dt / 1e6}
 
 
+def pmc_traffic(workload, launches_per_step):
+    """HBM bytes per inflate launch from the committed rocprofv3 PMC passes of this same command
+    (profiles/traffic.json, written by the profiling recipe in DESIGN.md), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("workload") != workload:
+        return None
+    return t.get("hbm_bytes_per_launch")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,7 +90,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=10000)
     ap.add_argument("--seg-records", type=int, default=2_621_440)   # ~1 GB of text per segment
     ap.add_argument("--repeats", type=int, default=203)             # per GPU: ~50 GB gz, ~532 M records
-    ap.add_argument("--out-capacity-gib", type=float, default=64.0)
+    ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -167,6 +181,8 @@ def main():
     launches = shard.batches * args.steps
     mean_launch_s = infl_ms / 1e3 / launches
     achieved = alg_local / shard.batches / mean_launch_s / 1e9
+    workload = ("configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000" if args.workload == "50gb"
+                else "configs[1]: 1 M-read .fastq.gz, chunk=10000")
     line = {
         "metric": "FASTQ records/sec + decompressed MB/s, 50 GB .fastq.gz, 1/2/4/8 MI355X",
         "value": rec_s,
@@ -180,14 +196,13 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)",
-        "config": {"workload": ("configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000" if args.workload == "50gb"
-                                else "configs[1]: 1 M-read .fastq.gz, chunk=10000"),
+        "config": {"workload": workload,
                    "records": total_records, "gz_bytes": tf.file_len, "decompressed_bytes": text_bytes,
                    "chunks": nchunks, "parallelism": f"chunk-sharded x{world}"},
         "decompressed_MBps": text_bytes * args.steps / elapsed / 1e6,
         "kernel_ms_per_step": {"inflate": infl_ms / args.steps, "parse": parse_ms / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload, shard.batches),
                      "kernel": "ppg_inflate_kernel", "alg_bytes_per_launch": alg_local / shard.batches,
                      "mean_launch_ms": mean_launch_s * 1e3},
         "reference_published_rec_s": REFERENCE_REC_S,
