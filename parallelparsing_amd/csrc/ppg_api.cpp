@@ -23,8 +23,8 @@
 #include "ppg_device.h"
 
 // launchers (ppg_inflate.hip, ppg_parse.hip)
-size_t ppg_inflate_lds_bytes(int ring_bits);
-hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, const uint32_t *comp, uint64_t nwords,
+size_t ppg_inflate_lds_bytes(int ring_bits, int lit_bits);
+hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
                               int njobs);
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
@@ -333,7 +333,8 @@ const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    int ring_bits = 11;   // inflate history ring: 2^11..2^15 bytes of LDS per wavefront (2 KiB: 24 waves/CU)
+    int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
+    int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)
 };
 
 namespace {
@@ -381,7 +382,9 @@ int ppg_open(int device, ppg_ctx **out) {
     auto ctx = std::make_unique<ppg_ctx>();
     ctx->device = device;
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-    if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(11, atoi(rb)));
+    if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(10, atoi(rb)));
+    if (const char *lb = getenv("PPG_LIT_BITS")) ctx->lit_bits = std::min(9, std::max(8, atoi(lb)));
+    if (ppg_inflate_lds_bytes(ctx->ring_bits, ctx->lit_bits) == 0) { ctx->ring_bits = 10; ctx->lit_bits = 8; }
     *out = ctx.release();
     return PPG_OK;
 }
@@ -543,7 +546,7 @@ int ppg_shard_run(ppg_shard *sh) {
     for (auto [b0, b1] : sh->batches) {
         const int nb = b1 - b0;
         HIPCHK(hipEventRecord(sh->ev[0], s));
-        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, (const uint32_t *)sh->comp, sh->nwords, sh->jobs.p + b0,
+        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords, sh->jobs.p + b0,
                                   sh->dicts.p, sh->out.p, sh->res.p + b0, nb));
         HIPCHK(hipEventRecord(sh->ev[1], s));
         HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,

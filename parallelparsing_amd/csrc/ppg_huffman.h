@@ -4,7 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define LB 9             // litlen root table bits (codes <= 9 bits: 99.9% of FASTQ tokens)
 #define DB 8             // distance root table bits
 #define CB 7             // code-length-code table bits (complete: max code length is 7)
 

@@ -28,12 +28,12 @@
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 
-template <int RB>
+template <int RB, int LBT>
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t ring[1u << RB];
     uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
     union {                        // the code-length code is dead once the litlen table is built
-        uint32_t lit[1 << LB];
+        uint32_t lit[1 << LBT];
         uint32_t cl[1 << CB];
     };
     uint32_t dst[1 << DB];
@@ -72,11 +72,21 @@ struct Reader {
     uint32_t bn;            // valid bits in bb
 };
 
+// global_load_lds_dword as inline asm: with the builtin the compiler waits for the DMA (vmcnt) before
+// every later LDS read that may alias the ring — each round would stall on the prefetch issued two
+// segments ahead and on any pending output stores.  Invisible to the compiler, the DMA is ordered
+// only by st_enter's explicit s_waitcnt; an untracked VMEM op can only make the compiler's own
+// vmcnt waits stricter, never looser.  (s_nop: SALU write of M0 -> LDS DMA needs one wait state.)
+__device__ __forceinline__ void lds_dma_dword(const uint32_t *src, const uint32_t *lds_base) {
+    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)lds_base)
+                 : "memory");
+}
+
 __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint32_t g, int lane) {
     const uint32_t i = min(g * 32 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
-    if (lane < 32) __builtin_amdgcn_global_load_lds(r.base + i, stream + (g & 3) * 32, 4, 0, 0);
-    // slot 0's first words again after slot 3, so a lane's three consecutive words never wrap
-    if ((g & 3) == 0 && lane < 4) __builtin_amdgcn_global_load_lds(r.base + i, stream + 128, 4, 0, 0);
+    if (lane < 32) lds_dma_dword(r.base + i, stream + (g & 3) * 32);
+    // slot 0's first words again after slot 3, so a lane's consecutive words never wrap
+    if ((g & 3) == 0 && lane < 4) lds_dma_dword(r.base + i, stream + 128);
 }
 
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
@@ -146,16 +156,20 @@ __device__ __forceinline__ void flush_range(const uint8_t *ring, uint8_t *out, u
 
 // Byte at chunk position p older than the ring: the flushed output (p >= 0; this wave's own
 // earlier stores — a wave's accesses to one address are ordered) or the Point's window.  Read as
-// an aligned dword so the compiler never merges it with an LDS byte load into one flat load.
-__device__ __forceinline__ uint32_t far_byte(const uint8_t *out, const uint8_t *dict, uint64_t out_off, int32_t p) {
-    const uint8_t *a = p >= 0 ? out + out_off + (uint32_t)p : dict + 32768 + p;   // p >= -32768
-    const uint32_t w = *(const uint32_t *)((uintptr_t)a & ~(uintptr_t)3);
-    return (w >> (8 * ((uintptr_t)a & 3))) & 255u;
+// an aligned dword from a uniform base + 32-bit lane offset (global_load saddr form; never merged
+// with an LDS byte load into a flat load).  ob: out + (out_off & ~3), oa: out_off & 3.
+__device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, const uint8_t *dict, int32_t p) {
+    // the two loads differ in width so the compiler cannot fold them into one per-lane base select
+    if (p >= 0) {
+        const uint32_t q = oa + (uint32_t)p;
+        return (*(const uint32_t *)(ob + (q & ~3u)) >> (8 * (q & 3))) & 255u;
+    }
+    return dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
 }
 
 // One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
 template <int RB>
-__device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, const uint8_t *dict, uint64_t out_off,
+__device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uint32_t oa, const uint8_t *dict,
                                            uint32_t rb0, uint32_t pos, uint32_t dist, uint32_t n, int lane) {
     constexpr uint32_t RM = (1u << RB) - 1;
     constexpr uint32_t REACH = (1u << RB) - 64;   // ring bytes a reference may use (see the emit)
@@ -185,7 +199,7 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, co
                 const int32_t rel = (int32_t)pos - (int32_t)back;
                 uint32_t v;
                 if (back + n <= REACH) v = ring[(dst0 - back) & RM];
-                else v = far_byte(out, dict, out_off, rel);
+                else v = far_byte(ob, oa, dict, rel);
                 ring[(dst0 + j) & RM] = (uint8_t)v;
             }
         }
@@ -194,13 +208,15 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *out, co
 
 // One speculative token from the 64 stream bits (lo, hi) at some bit offset, decoded with the
 // root tables.  Token word: [7:0] index of the next token's bit offset (this lane + its bits),
-// [16:8] output bytes (1: literal), [31:17] distance - 1 (match) or 0x400 | byte (literal: then
-// lane - 1 - field is negative and never "far", see the emit).  A special token (a code the
-// root tables do not resolve: end-of-block, invalid, long) is 255 | (0x400 | lane) << 17: next
+// [16:8] output bytes (1: literal), [31:17] distance - 1 (match) or 0x100 | byte (literal: then
+// lane - 1 - field lies in [-512, -194]: negative and, for any ring >= 1 KiB, never "far", see
+// the emit).  A special token (a code the root tables do not resolve: end-of-block, invalid,
+// long) is 255 | (0x100 | lane) << 17: next
 // index 255 ends the walk, 0 bytes.  Never 0 (the emit finds tokens by that).
+template <int LBT>
 __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32_t *dst, uint32_t lo, uint32_t hi,
                                                uint32_t lane) {
-    const uint32_t e = lit[lo & ((1u << LB) - 1)];
+    const uint32_t e = lit[lo & ((1u << LBT) - 1)];
     const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
     const uint32_t xb = (e >> 10) & 31;
     const uint32_t mlen = (e >> 16) + (r1 & ((1u << xb) - 1));
@@ -213,13 +229,13 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     const uint32_t tb = ((e >> 5) & 31) + (((d >> 5) & 31) & lm);
     const uint32_t nb = ((mlen - 1) & lm) + 1;                      // output bytes
     const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
-    const uint32_t field = ((dist - 1) & lm) | ((0x400u | (e >> 16)) & ~lm);
+    const uint32_t field = ((dist - 1) & lm) | ((0x100u | (e >> 16)) & ~lm);
     const uint32_t tok = (lane + tb) | (nb << 8) | (field << 17);
-    const uint32_t spec = 255u | ((0x400u | lane) << 17);
+    const uint32_t spec = 255u | ((0x100u | lane) << 17);
     return (tok & ~sm) | (spec & sm);
 }
 
-template <int RB>
+template <int RB, int LBT>
 __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
@@ -229,9 +245,9 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     // flush unit: far references (older than REACH = RING - 64) must already be flushed; a round
     // adds at most 64 + 258 bytes, so UNIT <= RING - 386 keeps them flushed (see copy_match)
     constexpr uint32_t UNIT = RB >= 13 ? 4096u : RING / 2;
-    static_assert(RB >= 11 && RB <= 15, "ring of 2..32 KiB");
+    static_assert(RB >= 10 && RB <= 15, "ring of 1..32 KiB");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    InflateLds<RB> &S = *reinterpret_cast<InflateLds<RB> *>(smem);
+    InflateLds<RB, LBT> &S = *reinterpret_cast<InflateLds<RB, LBT> *>(smem);
     const int lane = threadIdx.x;
     const int k = blockIdx.x;
     if (k >= njobs) return;
@@ -240,6 +256,8 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     const uint32_t len = (uint32_t)J.out_len;       // host guarantees < 2^31
     const uint32_t rb0 = (uint32_t)out_off;         // ring slot of chunk position p: (rb0 + p) & RM
     const uint8_t *dict = dicts + J.dict_off;       // chunk position p < 0 is dict[32768 + p]
+    const uint8_t *ob = out + (out_off & ~3ull);    // chunk position p >= 0 is ob[oa + p]
+    const uint32_t oa = (uint32_t)(out_off & 3);
 
     // history: the last RING bytes of the Point's window -> ring slots of positions [-RING, 0)
     for (uint32_t w0 = 0; w0 < RING / 4; w0 += 64) {
@@ -321,7 +339,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 S.lens[s] = L;
             }
             __syncthreads();
-            build_table<LB>(S.lens, 288, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane);
+            build_table<LBT>(S.lens, 288, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane);
             build_table<DB>(S.lens + 288, 32, S.dst, S.dst_count, S.dst_sorted, TAB_DST, lane);
         } else {
             // ---- dynamic Huffman codes (RFC 1951 3.2.7) ----
@@ -363,7 +381,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             __syncthreads();
             if (bad) { status = ST_DATA_ERROR; break; }
             if (uni(S.lens[256]) == 0) { status = ST_DATA_ERROR; break; }   // no end-of-block code
-            if (build_table<LB>(S.lens, (int)hlit, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane) != 0) { status = ST_DATA_ERROR; break; }
+            if (build_table<LBT>(S.lens, (int)hlit, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane) != 0) { status = ST_DATA_ERROR; break; }
             if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, S.dst_count, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
         }
         in_block = 1;
@@ -379,79 +397,87 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 
         // ---- token rounds ----
         uint32_t bp = rd_pos(r);
+        uint32_t cn = 0, cw = 0;   // carried: bytes left of the last round's last match, its token word
         while (pos < len) {
-            // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS ring)
-            st_enter(r, S.stream, bp >> 10, lane);
-            const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
-            const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
-            const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2], x3 = sw[3], x4 = sw[4];
-            // speculative tokens at every bit offset of the 128-bit span (two per lane)
-            const uint32_t vta = spec_token(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
-                                            __builtin_amdgcn_alignbit(x2, x1, o), (uint32_t)lane);
-            const uint32_t vtb = spec_token(S.lit, S.dst, __builtin_amdgcn_alignbit(x3, x2, o),
-                                            __builtin_amdgcn_alignbit(x4, x3, o), (uint32_t)lane);
-
-            // ---- walk the real token chain (wave-uniform): offset s -> s + bits(s) ----
-            // Each token goes to the lane of its output offset (vtin).  The walk runs through the
-            // first 64 offsets (vta), then the next 64 (vtb), and stops at a special token
-            // (recorded with 0 bytes, harmlessly), past the span, or once no further token can
-            // start inside the round's first min(64, len - pos) output bytes.
-            uint32_t s = 0, off = 0, t = 0, half = 0;
+            // A round emits at most 64 output bytes.  A match crossing that boundary is carried:
+            // its remaining bytes open the next round as a token at output offset 0.
+            uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t vtin = 0;
-            if (len - pos >= 64) {
-                do {
-                    t = rdlane(vta, s);
-                    vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                    off += (t >> 8) & 511u;
-                    s = t & 255u;
-                } while ((s | off) < 64u);
-                if (off < 64 && s != 255u) {   // crossed into the second 64 offsets
-                    s -= 64;
-                    half = 64;
+            if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
+            bool spec = false;
+            if (off < min(64u, len - pos)) {
+                // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS ring)
+                st_enter(r, S.stream, bp >> 10, lane);
+                const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
+                const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
+                const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2], x3 = sw[3], x4 = sw[4];
+                // speculative tokens at every bit offset of the 128-bit span (two per lane)
+                const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
+                                                     __builtin_amdgcn_alignbit(x2, x1, o), (uint32_t)lane);
+                const uint32_t vtb = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x3, x2, o),
+                                                     __builtin_amdgcn_alignbit(x4, x3, o), (uint32_t)lane);
+
+                // ---- walk the real token chain (wave-uniform): offset s -> s + bits(s) ----
+                // Each token goes to the lane of its output offset (vtin).  The walk runs through
+                // the first 64 offsets (vta), then the next 64 (vtb), and stops at a special token
+                // (recorded with 0 bytes, harmlessly), past the span, or once no further token can
+                // start inside the round's first min(64, len - pos) output bytes.
+                if (len - pos >= 64) {
                     do {
-                        t = rdlane(vtb, s);
+                        t = rdlane(vta, s);
                         vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
                         off += (t >> 8) & 511u;
                         s = t & 255u;
                     } while ((s | off) < 64u);
-                }
-            } else {
-                const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
-                do {
-                    t = rdlane(vta, s);
-                    vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                    off += (t >> 8) & 511u;
-                    s = t & 255u;
-                } while (max(s, off + cl) < 64u);
-                if (off + cl < 64 && s != 255u) {
-                    s -= 64;
-                    half = 64;
+                    if (off < 64 && s != 255u) {   // crossed into the second 64 offsets
+                        s -= 64;
+                        half = 64;
+                        do {
+                            t = rdlane(vtb, s);
+                            vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
+                            off += (t >> 8) & 511u;
+                            s = t & 255u;
+                        } while ((s | off) < 64u);
+                    }
+                } else {
+                    const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
                     do {
-                        t = rdlane(vtb, s);
+                        t = rdlane(vta, s);
                         vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
                         off += (t >> 8) & 511u;
                         s = t & 255u;
                     } while (max(s, off + cl) < 64u);
+                    if (off + cl < 64 && s != 255u) {
+                        s -= 64;
+                        half = 64;
+                        do {
+                            t = rdlane(vtb, s);
+                            vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
+                            off += (t >> 8) & 511u;
+                            s = t & 255u;
+                        } while (max(s, off + cl) < 64u);
+                    }
                 }
+                spec = s == 255u;
+                s = half + (spec ? ((t >> 17) & 63u) : s);   // bit offset of the next token
             }
-            const bool spec = s == 255u;
-            s = half + (spec ? ((t >> 17) & 63u) : s);   // bit offset of the next token
-            const uint32_t rout = min(off, len - pos);   // output bytes of this round
+            const uint32_t tot = min(off, len - pos);    // output bytes of the round's tokens
+            const uint32_t rout = min(tot, 64u);         // ... emitted this round
+            const uint64_t mo = __ballot(vtin != 0);     // token start offsets (never 0 words)
 
-            // ---- emit the round's first 64 output bytes, one per lane ----
+            // ---- emit the round's output bytes, one per lane ----
             // All 64 lanes write: lanes past rout leave garbage in the slots of positions
             // [pos + rout, pos + 64), which later rounds overwrite before use; the slots' previous
             // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
             // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
             {
-                const uint64_t mo = __ballot(vtin != 0);                              // token offsets
                 const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
                 const uint32_t inf = bperm(sj << 2, vtin);
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-                if (jj < -(int32_t)(RING - 64))                       // far (literals: jj > -1280)
-                    val = far_byte(out, dict, out_off, (int32_t)pos + jj);
+                if (jj < -(int32_t)(RING - 64))                       // far (literals: jj >= -512)
+                    val = far_byte(ob, oa, dict, (int32_t)pos + jj);
                 const bool dep = jj >= 0;                             // produced in this round
                 if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
@@ -465,11 +491,9 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 }
                 S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
             }
-            if (rout > 64) {
-                // the rest of the last token (a match): bytes 64.. of the round
-                const uint32_t lastt = 63u - (uint32_t)__builtin_clzll(__ballot(vtin != 0));
-                const uint32_t dl = (rdlane(vtin, lastt) >> 17) + 1;
-                copy_match<RB>(S.ring, out, dict, out_off, rb0, pos + 64, dl, rout - 64, lane);
+            cn = tot - rout;
+            if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
+                cw = rdlane(vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
             }
             pos += rout;
             if (pos >= fl_next) {
@@ -499,7 +523,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
                 const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
                 const uint32_t n = min(ml, len - pos);
-                copy_match<RB>(S.ring, out, dict, out_off, rb0, pos, ds, n, lane);
+                copy_match<RB>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
             }
             bp = rd_pos(r);
@@ -537,41 +561,27 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
 // ------------------------------------------------------------------------------------------
 // Host-side launcher (called from ppg_api.cpp).  ring_bits selects the history ring.
 // ------------------------------------------------------------------------------------------
-size_t ppg_inflate_lds_bytes(int ring_bits) {
-    switch (ring_bits) {
-        case 11: return sizeof(InflateLds<11>);
-        case 12: return sizeof(InflateLds<12>);
-        case 13: return sizeof(InflateLds<13>);
-        case 14: return sizeof(InflateLds<14>);
-        default: return sizeof(InflateLds<15>);
-    }
+// (ring bits, litlen root bits) variants; default (11, 9)
+#define PPG_VARIANTS(X) X(10, 8) X(10, 9) X(11, 9) X(11, 8) X(12, 9) X(12, 8) X(13, 9) X(15, 9)
+
+size_t ppg_inflate_lds_bytes(int ring_bits, int lit_bits) {
+#define X(R, L) if (ring_bits == R && lit_bits == L) return sizeof(InflateLds<R, L>);
+    PPG_VARIANTS(X)
+#undef X
+    return 0;
 }
 
-hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, const uint32_t *comp, uint64_t nwords,
+hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
                               int njobs) {
     if (njobs <= 0) return hipSuccess;
-    switch (ring_bits) {
-        case 11:
-            hipLaunchKernelGGL(ppg_inflate_kernel<11>, dim3(njobs), dim3(64), sizeof(InflateLds<11>), s, comp, nwords,
-                               jobs, dicts, out, res, njobs);
-            break;
-        case 12:
-            hipLaunchKernelGGL(ppg_inflate_kernel<12>, dim3(njobs), dim3(64), sizeof(InflateLds<12>), s, comp, nwords,
-                               jobs, dicts, out, res, njobs);
-            break;
-        case 13:
-            hipLaunchKernelGGL(ppg_inflate_kernel<13>, dim3(njobs), dim3(64), sizeof(InflateLds<13>), s, comp, nwords,
-                               jobs, dicts, out, res, njobs);
-            break;
-        case 14:
-            hipLaunchKernelGGL(ppg_inflate_kernel<14>, dim3(njobs), dim3(64), sizeof(InflateLds<14>), s, comp, nwords,
-                               jobs, dicts, out, res, njobs);
-            break;
-        default:
-            hipLaunchKernelGGL(ppg_inflate_kernel<15>, dim3(njobs), dim3(64), sizeof(InflateLds<15>), s, comp, nwords,
-                               jobs, dicts, out, res, njobs);
-            break;
+#define X(R, L)                                                                                               \
+    if (ring_bits == R && lit_bits == L) {                                                                    \
+        hipLaunchKernelGGL((ppg_inflate_kernel<R, L>), dim3(njobs), dim3(64), sizeof(InflateLds<R, L>), s, comp, \
+                           nwords, jobs, dicts, out, res, njobs);                                             \
+        return hipGetLastError();                                                                             \
     }
-    return hipGetLastError();
+    PPG_VARIANTS(X)
+#undef X
+    return hipErrorInvalidValue;
 }
