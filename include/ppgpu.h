@@ -129,6 +129,18 @@ int ppg_shard_counts_to_device(ppg_shard *sh, int64_t *dev_dst);
  * kernels only, and the whole run (ms). */
 int ppg_shard_timing(ppg_shard *sh, float *inflate_ms, float *parse_ms, float *total_ms);
 
+/* =============== DecompressAll from a .gz file: host ingest (LazyFileReader.cs:10-98) ===============
+ * Streams chunks [first, first+n) of gz_path through the GPU: `threads` reader threads (0 = 8)
+ * pread pieces of about piece_bytes compressed bytes (0 = 8 GiB: a launch needs thousands of
+ * chunks to fill the GPU) into pinned host buffers; a copy stream moves each piece to HBM and a
+ * helper thread prepares its jobs/windows while the previous piece decodes, so page cache, PCIe
+ * and the kernels overlap.  Buffers persist in the ctx across calls.  records[i] (may be NULL) receives chunk first+i's record count,
+ * *total_records their sum, *seconds the wall time from the first read to the last result.
+ * Returns 0, PPG_IO_ERROR for an unreadable file, or the first chunk error (ZResult code). */
+int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
+                            int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,
+                            double *seconds);
+
 /* Library build string (kernel ISA, version). */
 const char *ppg_version(void);
 

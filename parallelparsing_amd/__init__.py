@@ -333,6 +333,23 @@ class Shard:
         return {"inflate_ms": a.value, "parse_ms": b.value, "total_ms": c.value}
 
 
+def decompress_file(index, gzip_path, first=0, n=None, piece_bytes=8 << 30, threads=8, device=None):
+    """DecompressAll of chunks [first, first+n) straight from a .gz file (ppg_file_decompress_all):
+    reader threads pread ~piece_bytes pieces into pinned buffers, H2D overlaps the decode of the
+    previous piece (the LazyFileReader path, Decompressor/LazyFileReader.cs:10-98).
+    Returns (per-chunk record counts, total records, wall seconds)."""
+    dev = device or Device.default()
+    if n is None:
+        n = index.Count - 1 - first
+    rec = np.zeros(max(n, 1), np.int64)
+    tot = C.c_int64(0)
+    sec = C.c_double(0)
+    check(lib.ppg_file_decompress_all(dev.handle, index.handle, os.fsencode(gzip_path), int(first), int(n),
+                                      int(piece_bytes), int(threads), _ptr(rec), C.byref(tot), C.byref(sec)),
+          "decompress_file")
+    return rec[:n], tot.value, sec.value
+
+
 class BatchedFASTQ:
     """Decompressor/BatchedFASTQ.cs:10-101 — DecompressAll as an iterable of FastqRecord.
 
@@ -361,7 +378,13 @@ class BatchedFASTQ:
         return self._shard
 
     def Count(self):
-        return self._run().total_records
+        """Number of records (Enumerable.Count over the enumerator, Decompressor/Program.cs:48-52):
+        streamed from the file, nothing materialised on the host."""
+        if self._shard is not None:
+            return self._shard.total_records
+        _, total, _ = decompress_file(self.index, self.gzip_path, device=self.dev,
+                                      threads=16 if self.enable_ssd_optimization else 8)
+        return total
 
     def __iter__(self):
         sh = self._run()

@@ -5,6 +5,8 @@
 //   ppg_ctx                        one GPU, one HIP stream
 //   ppg_shard                      DecompressAll over chunks [first, first+n): device-resident
 //                                  compressed range + windows + offsets, batched inflate + parse
+//   ppg_file_decompress_all        host ingest (LazyFileReader.cs:10-98): pread into pinned
+//                                  buffers, H2D on a copy stream overlapped with decoding
 //
 // No CPU fallback exists for the decode: without a usable gfx950 device every decode entry point
 // returns PPG_NO_DEVICE / PPG_DEVICE_ERROR.
@@ -18,6 +20,12 @@
 #include <string>
 #include <algorithm>
 #include <memory>
+#include <thread>
+#include <mutex>
+#include <condition_variable>
+#include <chrono>
+#include <fcntl.h>
+#include <unistd.h>
 
 #include "../../include/ppgpu.h"
 #include "ppg_device.h"
@@ -53,13 +61,16 @@ struct PpgPoint {                       // Common/Index.cs:51-82
     int64_t output = 0;                 // offset in the uncompressed stream
     int64_t input = 0;                  // offset of the first full byte in the .gz
     int32_t bits = 0;                   // unused bits (1-7) of byte input-1, or 0
-    std::vector<uint8_t> window;        // the preceding 32 KiB of output, oldest first
     std::vector<uint8_t> offset;        // bytes since the last '@' (the partial record)
 };
 
 struct ppg_index {
     int32_t chunk_max_bytes = 0;
     std::vector<PpgPoint> pts;
+    // Point.Window (the preceding 32 KiB of output, oldest first) of point i at i * kWin: one
+    // contiguous array, so a range of chunks ships its windows to the GPU in one copy
+    std::vector<uint8_t> windows;
+    const uint8_t *win(size_t i) const { return windows.data() + i * kWin; }
 
     // Index.AddPoint (Common/Index.cs:24-48)
     void add_point(int bits, int64_t input, int64_t output, uint32_t left, const uint8_t *circ,
@@ -74,10 +85,11 @@ struct ppg_index {
         p.output = output;
         p.input = input;
         p.bits = bits;
-        p.window.resize(kWin);
         // oldest bytes (those after the circular write head) first
-        std::copy(circ + (kWin - left), circ + kWin, p.window.begin());
-        std::copy(circ, circ + (kWin - left), p.window.begin() + left);
+        const size_t w0 = windows.size();
+        windows.resize(w0 + kWin);
+        std::copy(circ + (kWin - left), circ + kWin, windows.begin() + w0);
+        std::copy(circ, circ + (kWin - left), windows.begin() + w0 + left);
         p.offset.assign(off, off + off_len);
         pts.push_back(std::move(p));
     }
@@ -238,10 +250,11 @@ int ppg_index_serialize(const ppg_index *ix, const char *path) {
     bool ok = true;
     const int32_t hdr[3] = {0, ix->chunk_max_bytes, (int32_t)ix->pts.size()};
     ok &= write_all(f, hdr, sizeof hdr);
-    for (const auto &p : ix->pts) {
-        const int32_t wl = (int32_t)p.window.size(), ol = (int32_t)p.offset.size();
+    for (size_t i = 0; i < ix->pts.size(); i++) {
+        const auto &p = ix->pts[i];
+        const int32_t wl = kWin, ol = (int32_t)p.offset.size();
         ok &= write_all(f, &p.output, 8) && write_all(f, &p.input, 8) && write_all(f, &p.bits, 4);
-        ok &= write_all(f, &wl, 4) && write_all(f, p.window.data(), p.window.size());
+        ok &= write_all(f, &wl, 4) && write_all(f, ix->win(i), kWin);
         ok &= write_all(f, &ol, 4) && write_all(f, p.offset.data(), p.offset.size());
     }
     ok &= fclose(f) == 0;
@@ -256,18 +269,20 @@ int ppg_index_deserialize(const char *path, ppg_index **out) {
     auto ix = std::make_unique<ppg_index>();
     int32_t hdr[3];
     bool ok = read_all(f, hdr, sizeof hdr) && hdr[2] >= 0;
+    std::vector<uint8_t> wbuf;
     for (int32_t i = 0; ok && i < hdr[2]; i++) {
         PpgPoint p;
         int32_t wl = 0, ol = 0;
         ok = read_all(f, &p.output, 8) && read_all(f, &p.input, 8) && read_all(f, &p.bits, 4) && read_all(f, &wl, 4) &&
              wl >= 0;
         if (!ok) break;
-        p.window.resize((size_t)wl);
-        ok = read_all(f, p.window.data(), (size_t)wl) && read_all(f, &ol, 4) && ol >= 0;
+        wbuf.assign((size_t)std::max(wl, kWin), 0);
+        ok = read_all(f, wbuf.data(), (size_t)wl) && read_all(f, &ol, 4) && ol >= 0;
         if (!ok) break;
         p.offset.resize((size_t)ol);
         ok = read_all(f, p.offset.data(), (size_t)ol);
-        if (wl < kWin) p.window.resize(kWin, 0);
+        // inflateSetDictionary(Window, 32768) (Core.cs:158) uses the first 32 KiB
+        ix->windows.insert(ix->windows.end(), wbuf.begin(), wbuf.begin() + kWin);
         ix->pts.push_back(std::move(p));
     }
     fclose(f);
@@ -284,13 +299,13 @@ int ppg_index_from_points(int32_t count, const int64_t *output, const int64_t *i
     auto ix = std::make_unique<ppg_index>();
     ix->chunk_max_bytes = chunk_max_bytes;
     ix->pts.resize((size_t)count);
+    ix->windows.assign(windows, windows + (size_t)count * kWin);
     size_t o = 0;
     for (int32_t i = 0; i < count; i++) {
         PpgPoint &p = ix->pts[(size_t)i];
         p.output = output[i];
         p.input = input[i];
         p.bits = bits[i];
-        p.window.assign(windows + (size_t)i * kWin, windows + (size_t)(i + 1) * kWin);
         if (offset_len[i] < 0) return PPG_ARG_ERROR;
         p.offset.assign(offsets + o, offsets + o + offset_len[i]);
         o += (size_t)offset_len[i];
@@ -315,7 +330,7 @@ int ppg_index_point(const ppg_index *ix, int32_t i, int64_t *output, int64_t *in
 
 const uint8_t *ppg_index_window(const ppg_index *ix, int32_t i) {
     if (!ix || i < 0 || (size_t)i >= ix->pts.size()) return nullptr;
-    return ix->pts[(size_t)i].window.data();
+    return ix->win((size_t)i);
 }
 
 const uint8_t *ppg_index_offset(const ppg_index *ix, int32_t i) {
@@ -330,9 +345,12 @@ const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate
 }  // extern "C"
 
 // ====================================== device ======================================
+struct IngestState;   // host-ingest buffers kept across ppg_file_decompress_all calls
+
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    IngestState *ingest = nullptr;
     int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
     int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)
 };
@@ -349,6 +367,18 @@ struct DevBuf {
         if (p) { (void)hipFree(p); p = nullptr; }
         n = count;
         return hipMalloc((void **)&p, std::max<size_t>(count, 1) * sizeof(T));
+    }
+};
+
+struct PinnedBuf {
+    uint8_t *p = nullptr;
+    size_t n = 0;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t alloc(size_t count) {
+        if (p && n >= count) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; }
+        n = count;
+        return hipHostMalloc((void **)&p, std::max<size_t>(count, 1), hipHostMallocDefault);
     }
 };
 
@@ -389,9 +419,14 @@ int ppg_open(int device, ppg_ctx **out) {
     return PPG_OK;
 }
 
+}  // extern "C"
+static void ingest_free(IngestState *st);
+extern "C" {
+
 void ppg_close(ppg_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    ingest_free(ctx->ingest);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -441,40 +476,35 @@ void ppg_shard_free(ppg_shard *sh) {
     delete sh;
 }
 
-int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n, const void *comp, int64_t comp_len,
-                     int comp_on_device, int64_t out_capacity, ppg_shard **out) {
-    if (!ctx || !ix || !comp || !out || n < 0 || first < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
-        return PPG_ARG_ERROR;
+}  // extern "C"
+
+// (Re)build a shard's per-chunk state for chunks [first, first+n) whose compressed range
+// [Index[first].Input-1, Index[first+n].Input-1] is at device pointer comp (4-byte aligned,
+// readable 64 bytes past comp_len).  Device buffers are reused when large enough, so a shard can
+// be re-prepared piece after piece (ppg_file_decompress_all).
+static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, const uint8_t *comp,
+                         int64_t comp_len, int64_t out_capacity, hipStream_t s) {
     const auto &P = ix->pts;
     const int64_t base_byte = P[(size_t)first].input - 1;
     if (base_byte < 0) return PPG_ARG_ERROR;
     if (comp_len != P[(size_t)first + n].input - P[(size_t)first].input + 1) return PPG_ARG_ERROR;
-    HIPCHK(hipSetDevice(ctx->device));
-    auto sh = std::unique_ptr<ppg_shard, void (*)(ppg_shard *)>(new ppg_shard, ppg_shard_free);
-    sh->ctx = ctx;
+    if (((uintptr_t)comp & 3) != 0) return PPG_ARG_ERROR;
     sh->first = first;
     sh->n = n;
+    sh->comp = comp;
     sh->comp_len = comp_len;
     sh->nwords = (uint64_t)(comp_len + 3) / 4;
-    hipStream_t s = ctx->stream;
-    if (comp_on_device) {
-        if (((uintptr_t)comp & 3) != 0) return PPG_ARG_ERROR;
-        sh->comp = (const uint8_t *)comp;
-    } else {
-        HIPCHK(sh->comp_own.alloc((size_t)comp_len + 64));
-        HIPCHK(hipMemsetAsync(sh->comp_own.p + comp_len, 0, 64, s));
-        HIPCHK(hipMemcpyAsync(sh->comp_own.p, comp, (size_t)comp_len, hipMemcpyHostToDevice, s));
-        sh->comp = sh->comp_own.p;
-    }
+    sh->ran = 0;
+    sh->batches.clear();
     // batches: consecutive chunks whose outputs fit out_capacity (0 = everything at once)
     int64_t total_out = P[(size_t)first + n].output - P[(size_t)first].output;
     if (total_out < 0) return PPG_ARG_ERROR;
     int64_t cap = out_capacity > 0 ? out_capacity : total_out;
     sh->h_jobs.resize((size_t)n);
+    int64_t need_max = 0;
     {
         int32_t b0 = 0;
         int64_t bbase = P[(size_t)first].output;
-        int64_t need_max = 0;
         for (int32_t i = 0; i < n; i++) {
             const PpgPoint &from = P[(size_t)first + i], &to = P[(size_t)first + i + 1];
             int64_t ulen = to.output - from.output;
@@ -497,24 +527,22 @@ int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n
             sh->batches.push_back({b0, n});
             need_max = std::max(need_max, P[(size_t)first + n].output - bbase);
         }
-        sh->out_cap = std::max<int64_t>(need_max, 0);
     }
+    const int64_t out_cap = std::max<int64_t>(need_max, 0);
     HIPCHK(sh->jobs.alloc((size_t)n));
     HIPCHK(hipMemcpyAsync(sh->jobs.p, sh->h_jobs.data(), sizeof(PpgInflateJob) * (size_t)n, hipMemcpyHostToDevice, s));
-    // windows and offsets of the shard's `from` points
-    std::vector<uint8_t> hwin((size_t)n * kWin);
+    // windows (contiguous in the index) and offsets of the shard's `from` points
+    if (ix->windows.size() < ((size_t)first + n) * kWin) return PPG_ARG_ERROR;
     std::vector<PpgOffsetRef> horef((size_t)n);
     std::vector<uint8_t> hoff;
     for (int32_t i = 0; i < n; i++) {
         const PpgPoint &from = P[(size_t)first + i];
-        if (from.window.size() < (size_t)kWin) return PPG_ARG_ERROR;
-        memcpy(hwin.data() + (size_t)i * kWin, from.window.data(), kWin);
         horef[(size_t)i].start = hoff.size();
         horef[(size_t)i].len = (uint32_t)from.offset.size();
         hoff.insert(hoff.end(), from.offset.begin(), from.offset.end());
     }
-    HIPCHK(sh->dicts.alloc(hwin.size()));
-    HIPCHK(hipMemcpyAsync(sh->dicts.p, hwin.data(), hwin.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(sh->dicts.alloc((size_t)n * kWin));
+    HIPCHK(hipMemcpyAsync(sh->dicts.p, ix->win((size_t)first), (size_t)n * kWin, hipMemcpyHostToDevice, s));
     HIPCHK(sh->offs.alloc(hoff.size() + 16));
     if (!hoff.empty()) HIPCHK(hipMemcpyAsync(sh->offs.p, hoff.data(), hoff.size(), hipMemcpyHostToDevice, s));
     HIPCHK(sh->oref.alloc((size_t)n));
@@ -524,13 +552,37 @@ int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n
     HIPCHK(sh->base.alloc((size_t)n));
     HIPCHK(sh->total.alloc(1));
     // output + a 64-byte tail: the parse kernels read whole 16-B words
-    HIPCHK(sh->out.alloc((size_t)sh->out_cap + 64));
-    HIPCHK(hipMemsetAsync(sh->out.p + sh->out_cap, 0, 64, s));
+    if ((size_t)out_cap + 64 > sh->out.n) HIPCHK(sh->out.alloc((size_t)out_cap + 64));
+    sh->out_cap = (int64_t)sh->out.n - 64;
+    HIPCHK(hipMemsetAsync(sh->out.p + out_cap, 0, 64, s));
     // descriptor space (16 B per record) sized for >= 256-B records; a batch that needs more
     // grows it before its emit pass (ppg_shard_run)
-    HIPCHK(sh->recs.alloc((size_t)(4 * (sh->out_cap / 256 + 1024))));
-    for (auto &e : sh->ev) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(sh->recs.alloc((size_t)(4 * (out_cap / 256 + 1024))));
+    if (!sh->ev[0])
+        for (auto &e : sh->ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipStreamSynchronize(s));   // the host staging vectors above die here
+    return PPG_OK;
+}
+
+extern "C" {
+
+int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n, const void *comp, int64_t comp_len,
+                     int comp_on_device, int64_t out_capacity, ppg_shard **out) {
+    if (!ctx || !ix || !comp || !out || n < 0 || first < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
+        return PPG_ARG_ERROR;
+    HIPCHK(hipSetDevice(ctx->device));
+    auto sh = std::unique_ptr<ppg_shard, void (*)(ppg_shard *)>(new ppg_shard, ppg_shard_free);
+    sh->ctx = ctx;
+    const uint8_t *dcomp = (const uint8_t *)comp;
+    if (!comp_on_device) {
+        hipStream_t s = ctx->stream;
+        HIPCHK(sh->comp_own.alloc((size_t)comp_len + 64));
+        HIPCHK(hipMemsetAsync(sh->comp_own.p + comp_len, 0, 64, s));
+        HIPCHK(hipMemcpyAsync(sh->comp_own.p, comp, (size_t)comp_len, hipMemcpyHostToDevice, s));
+        dcomp = sh->comp_own.p;
+    }
+    const int rc = shard_prepare(sh.get(), ix, first, n, dcomp, comp_len, out_capacity, ctx->stream);
+    if (rc != PPG_OK) return rc;
     *out = sh.release();
     return PPG_OK;
 }
@@ -670,6 +722,192 @@ int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uin
         if (rc == PPG_OK) rc = ppg_shard_copy_records(sh, 0, recs, rec_cap, nrec);
     }
     ppg_shard_free(sh);
+    return rc;
+}
+
+}  // extern "C"
+
+// ================================ host ingest (file -> GPU) ================================
+namespace {
+
+// pread [off, off+len) of fd into dst with `threads` parallel readers; false on a short read
+bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads) {
+    const int64_t part = std::max<int64_t>((len + threads - 1) / threads, 1 << 20);
+    std::vector<std::thread> th;
+    std::vector<int> ok;
+    const int nparts = (int)std::max<int64_t>(1, (len + part - 1) / part);
+    ok.assign((size_t)nparts, 1);
+    for (int t = 0; t < nparts; t++) {
+        th.emplace_back([=, &ok] {
+            int64_t a = (int64_t)t * part, b = std::min(len, a + part);
+            while (a < b) {
+                const ssize_t r = pread(fd, dst + a, (size_t)(b - a), off + a);
+                if (r <= 0) { ok[(size_t)t] = 0; return; }
+                a += r;
+            }
+        });
+    }
+    for (auto &x : th) x.join();
+    for (int v : ok) if (!v) return false;
+    return true;
+}
+
+}  // namespace
+
+constexpr int kSlots = 4;                        // pinned staging slots
+constexpr int64_t kSlotBytes = (int64_t)128 << 20;
+
+struct IngestState {
+    PinnedBuf slot[kSlots];       // pinned host staging, streamed through round-robin
+    hipEvent_t slot_ev[kSlots] = {};
+    DevBuf<uint8_t> db[2];        // device copies of two pieces (one decoding, one filling)
+    hipStream_t cs = nullptr;     // copy stream
+    ppg_shard *sh[2] = {nullptr, nullptr};
+};
+
+static void ingest_free(IngestState *st) {
+    if (!st) return;
+    for (int i = 0; i < kSlots; i++)
+        if (st->slot_ev[i]) (void)hipEventDestroy(st->slot_ev[i]);
+    for (int i = 0; i < 2; i++)
+        if (st->sh[i]) ppg_shard_free(st->sh[i]);
+    if (st->cs) (void)hipStreamDestroy(st->cs);
+    delete st;
+}
+
+extern "C" {
+
+int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
+                            int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,
+                            double *seconds) {
+    if (!ctx || !ix || !gz_path || n < 0 || first < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
+        return PPG_ARG_ERROR;
+    const auto &P = ix->pts;
+    if (piece_bytes <= 0) piece_bytes = (int64_t)8 << 30;   // ~8k chunks at chunk=10000: one full wave generation
+    if (threads <= 0) threads = 8;
+    const bool verbose = getenv("PPG_INGEST_VERBOSE") != nullptr;
+    HIPCHK(hipSetDevice(ctx->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    auto now_ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    const int fd = open(gz_path, O_RDONLY);
+    if (fd < 0) return PPG_IO_ERROR;
+    struct FdClose { int fd; ~FdClose() { close(fd); } } fdc{fd};
+
+    // pieces: consecutive chunks of about piece_bytes compressed bytes (at least one chunk)
+    std::vector<std::pair<int32_t, int32_t>> pieces;
+    int64_t maxlen = 0;
+    for (int32_t a = 0; a < n;) {
+        int32_t b = a + 1;
+        while (b < n && P[(size_t)first + b + 1].input - P[(size_t)first + a].input + 1 <= piece_bytes) b++;
+        pieces.push_back({a, b});
+        maxlen = std::max(maxlen, P[(size_t)first + b].input - P[(size_t)first + a].input + 1);
+        a = b;
+    }
+    auto range = [&](size_t k, int64_t &off, int64_t &len) {
+        off = P[(size_t)first + pieces[k].first].input - 1;
+        len = P[(size_t)first + pieces[k].second].input - P[(size_t)first + pieces[k].first].input + 1;
+    };
+
+    // buffers persist in the ctx across calls (pinning and device allocation are slow)
+    if (!ctx->ingest) {
+        auto st = new IngestState;
+        ctx->ingest = st;
+        HIPCHK(hipStreamCreateWithFlags(&st->cs, hipStreamNonBlocking));
+        for (int i = 0; i < kSlots; i++) {
+            HIPCHK(hipEventCreateWithFlags(&st->slot_ev[i], hipEventDisableTiming));
+            HIPCHK(st->slot[i].alloc((size_t)kSlotBytes));
+        }
+        for (int i = 0; i < 2; i++) {
+            st->sh[i] = new ppg_shard;
+            st->sh[i]->ctx = ctx;
+        }
+    }
+    IngestState &S = *ctx->ingest;
+    for (int i = 0; i < 2; i++) HIPCHK(S.db[i].alloc((size_t)maxlen + 64));
+    if (verbose) fprintf(stderr, "[ingest] %zu pieces, max %.1f MB, setup %.1f ms\n", pieces.size(), maxlen / 1e6, now_ms());
+
+    // Producer thread: piece k -> device buffer k&1 (pread into pinned slots, H2D on the copy
+    // stream, slot by slot), then its jobs/windows/offsets (shard_prepare, which syncs the copy
+    // stream).  Consumer (this thread): decodes piece k once ready.  At most two pieces in flight.
+    const size_t np = pieces.size();
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t ready = 0, done = 0;
+    int prod_rc = PPG_OK;
+    bool stop = false;
+    auto producer = [&] {
+        (void)hipSetDevice(ctx->device);
+        int rcp = PPG_OK;
+        size_t slot = 0;
+        for (size_t k = 0; k < np && rcp == PPG_OK; k++) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || k < done + 2; });
+                if (stop) return;
+            }
+            const double t1 = now_ms();
+            int64_t off, len;
+            range(k, off, len);
+            uint8_t *dst = S.db[k & 1].p;
+            for (int64_t r = 0; r < len && rcp == PPG_OK; r += kSlotBytes, slot = (slot + 1) % kSlots) {
+                const int64_t m = std::min(kSlotBytes, len - r);
+                if (hipEventSynchronize(S.slot_ev[slot]) != hipSuccess) { rcp = PPG_DEVICE_ERROR; break; }
+                if (!pread_parallel(fd, S.slot[slot].p, off + r, m, threads)) { rcp = PPG_IO_ERROR; break; }
+                if (hipMemcpyAsync(dst + r, S.slot[slot].p, (size_t)m, hipMemcpyHostToDevice, S.cs) != hipSuccess ||
+                    hipEventRecord(S.slot_ev[slot], S.cs) != hipSuccess)
+                    rcp = PPG_DEVICE_ERROR;
+            }
+            const double t2 = now_ms();
+            if (rcp == PPG_OK && hipMemsetAsync(dst + len, 0, 64, S.cs) != hipSuccess) rcp = PPG_DEVICE_ERROR;
+            if (rcp == PPG_OK)
+                rcp = shard_prepare(S.sh[k & 1], ix, first + pieces[k].first, pieces[k].second - pieces[k].first, dst,
+                                    len, 0, S.cs);
+            if (verbose)
+                fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms, prepare %.1f ms\n", k,
+                        len / 1e6, t1, t2 - t1, now_ms() - t2);
+            std::lock_guard<std::mutex> lk(mu);
+            if (rcp != PPG_OK) prod_rc = rcp;
+            else ready = k + 1;
+            cv.notify_all();
+        }
+    };
+    std::thread prod(producer);
+    struct Joiner {
+        std::thread &t; std::mutex &m; std::condition_variable &c; bool &stop;
+        ~Joiner() { { std::lock_guard<std::mutex> lk(m); stop = true; } c.notify_all(); if (t.joinable()) t.join(); }
+    } joiner{prod, mu, cv, stop};
+
+    int64_t total = 0;
+    int rc = PPG_OK;
+    for (size_t k = 0; k < np; k++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return ready > k || prod_rc != PPG_OK; });
+            if (ready <= k) { rc = prod_rc; break; }
+        }
+        const int32_t a = pieces[k].first, b = pieces[k].second;
+        const double tr = now_ms();
+        rc = ppg_shard_run(S.sh[k & 1]);
+        if (verbose)
+            fprintf(stderr, "[ingest] piece %zu: %d chunks, run at %.1f ms in %.1f ms (kernels %.1f)\n", k, b - a, tr,
+                    now_ms() - tr, S.sh[k & 1]->t_total);
+        if (rc == PPG_OK || S.sh[k & 1]->ran) {
+            for (int32_t i = 0; i < b - a; i++) {
+                const int64_t r = (int64_t)S.sh[k & 1]->h_info[(size_t)i].records;
+                if (records) records[a + i] = r;
+                total += r;
+            }
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        done = k + 1;
+        cv.notify_all();
+        if (rc != PPG_OK) break;
+    }
+    hipStream_t cs = S.cs;
+    HIPCHK(hipStreamSynchronize(cs));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (total_records) *total_records = total;
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return rc;
 }
 

@@ -143,3 +143,56 @@ def test_larger_file_vs_oracle_and_trailer(device):
         tot += len(rec)
     assert crc == int.from_bytes(gz[-8:-4], "little")
     assert tot == sh.total_records == nrec   # zlib -6 never places a Point at a record start here
+
+
+@pytest.mark.parametrize("name,piece", [("l6_c20", 1), ("memlevel1_c10", 20000), ("stored_c50", 1),
+                                        ("pigz_c100", 1 << 30), ("huffonly_c20", 50000)])
+def test_file_ingest_matches_golden(name, piece, tmp_path, device):
+    """Host ingest (ppg_file_decompress_all, the LazyFileReader path): pieces as small as one
+    chunk stream through pinned buffers + a copy stream; per-chunk record counts == fixtures."""
+    meta, gz = load_case(name)
+    p = tmp_path / "f.gz"
+    p.write_bytes(gz)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    rec, tot, sec = pp.decompress_file(ix, str(p), piece_bytes=piece, threads=3, device=device)
+    assert [int(x) for x in rec] == [c["records"] for c in meta["chunks"]]
+    assert tot == meta["total_records"] and sec > 0
+    # a sub-range of the chunks
+    if ix.Count > 4:
+        rec2, tot2, _ = pp.decompress_file(ix, str(p), first=1, n=ix.Count - 3, piece_bytes=piece, device=device)
+        assert [int(x) for x in rec2] == [c["records"] for c in meta["chunks"][1:ix.Count - 2]]
+
+
+def test_file_ingest_errors(tmp_path, device):
+    meta, gz = load_case("l6_c20")
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    with pytest.raises(pp.PpgError) as e:
+        pp.decompress_file(ix, str(tmp_path / "missing.gz"), device=device)
+    assert e.value.code == -51   # PPG_IO_ERROR
+    # a truncated file: the read of the last piece comes up short
+    p = tmp_path / "t.gz"
+    p.write_bytes(gz[: len(gz) // 2])
+    with pytest.raises(pp.PpgError) as e:
+        pp.decompress_file(ix, str(p), piece_bytes=1, device=device)
+    assert e.value.code == -51
+
+
+def test_file_ingest_large_vs_oracle(tmp_path, device):
+    """200k records through 4 MB pieces: counts == the oracle's threaded DecompressAll."""
+    import ctypes as C
+    S = pp.synth()
+    nrec = 200_000
+    sz = S.ppg_synth_fastq_size(0, nrec, 150)
+    txt = np.zeros(sz, np.uint8)
+    S.ppg_synth_fastq(7, 0, nrec, 150, C.c_void_p(txt.ctypes.data), sz, 8)
+    gzb = np.zeros(sz, np.uint8)
+    L = S.ppg_synth_gzip(C.c_void_p(txt.ctypes.data), sz, 6, 4 << 20, 8, C.c_void_p(gzb.ctypes.data), gzb.size)
+    gz = gzb[:L].tobytes()
+    p = tmp_path / "big.gz"
+    p.write_bytes(gz)
+    ix = pp.Core.BuildDeflateIndex(str(p), 10000)
+    rec, tot, _ = pp.decompress_file(ix, str(p), piece_bytes=4 << 20, threads=4, device=device)
+    oi = O.build_index(gz, 10000)
+    exp_tot, _ = O.decompress_all(gz, oi, threads=8)
+    assert tot == exp_tot == nrec
+    assert pp.BatchedFASTQ(ix, str(p), True, device=device).Count() == nrec
