@@ -121,6 +121,12 @@ int ppg_shard_copy_chunk(ppg_shard *sh, int32_t k, uint8_t *dst, int64_t cap, in
 int ppg_shard_copy_records(ppg_shard *sh, int32_t k, uint32_t *dst, int64_t cap, int64_t *nrec);
 int ppg_shard_record_base(ppg_shard *sh, int64_t *base); /* n record bases (exclusive scan) */
 
+/* Paired reads (the reference only names the goal, README.md:9): the spot number
+ * of every record of a one-batch shard, in record order, into caller device memory (cap int64s):
+ * the digits between the first two '.' of the Identifier ("SRR<id>.<spot>.<mate> ..."), -1 when
+ * absent, -2 for a record the reference parses twice, which a pairing drops. */
+int ppg_shard_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap);
+
 /* Device-resident per-chunk record counts (int64[n]) copied to caller device memory on this
  * GPU (the input of the cross-GPU all-gather). */
 int ppg_shard_counts_to_device(ppg_shard *sh, int64_t *dev_dst);

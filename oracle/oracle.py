@@ -65,8 +65,9 @@ class OracleIndex:
         self.h = C.c_void_p(h)
 
     def __del__(self):
-        if getattr(self, "h", None) is not None and self.h.value:
+        if getattr(self, "h", None) is not None and self.h.value and L is not None:   # L is None at exit
             L.orc_index_free(self.h)
+            self.h = None
 
     @property
     def count(self):

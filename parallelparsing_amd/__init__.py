@@ -285,6 +285,10 @@ class Shard:
             lib.ppg_shard_free(h)
             self._h = None
 
+    @property
+    def handle(self):
+        return self._h
+
     def run(self):
         check(lib.ppg_shard_run(self._h), "DecompressAll")
         return self

@@ -47,6 +47,14 @@ def _load(path, what):
     return C.CDLL(path)
 
 
+# One HIP runtime per process: torch (when present) bundles its own libamdhip64 with the same soname
+# as /opt/rocm's.  Whichever loads first serves both, and torch fails to initialise the GPU on the
+# other's.  Importing torch first makes libppgpu bind to torch's runtime, as in bench.py.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 lib = _load(LIB_PATH, "libppgpu.so")
 
 vp = C.c_void_p
@@ -79,6 +87,7 @@ _SIGS = {
     "ppg_shard_copy_chunk": (C.c_int, [vp, i32, vp, i64, P(i64)]),
     "ppg_shard_copy_records": (C.c_int, [vp, i32, vp, i64, P(i64)]),
     "ppg_shard_record_base": (C.c_int, [vp, vp]),
+    "ppg_shard_keys": (C.c_int, [vp, vp, i64]),
     "ppg_shard_counts_to_device": (C.c_int, [vp, vp]),
     "ppg_shard_timing": (C.c_int, [vp, P(C.c_float), P(C.c_float), P(C.c_float)]),
     "ppg_file_decompress_all": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, vp, P(i64), P(C.c_double)]),
@@ -103,6 +112,10 @@ def synth():
         s.ppg_synth_fastq_size.argtypes = [i64, i64, C.c_int]
         s.ppg_synth_fastq.restype = i64
         s.ppg_synth_fastq.argtypes = [C.c_uint64, i64, i64, C.c_int, vp, i64, C.c_int]
+        s.ppg_synth_fastq_size_mate.restype = i64
+        s.ppg_synth_fastq_size_mate.argtypes = [i64, i64, C.c_int, C.c_int]
+        s.ppg_synth_fastq_mate.restype = i64
+        s.ppg_synth_fastq_mate.argtypes = [C.c_uint64, C.c_int, i64, i64, C.c_int, vp, i64, C.c_int]
         s.ppg_synth_gzip.restype = i64
         s.ppg_synth_gzip.argtypes = [vp, i64, C.c_int, i64, C.c_int, vp, i64]
         s.ppg_synth_segment.restype = i64

@@ -41,6 +41,10 @@ hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgIn
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                  PpgParseInfo *info, const uint64_t *base, uint32_t *recs, int n);
+hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
+                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
+                                  const PpgParseInfo *info, const uint64_t *base, const uint32_t *recs, int64_t *keys,
+                                  int n);
 
 #define HIPCHK(x)                                                                          \
     do {                                                                                   \
@@ -679,6 +683,17 @@ int ppg_shard_copy_records(ppg_shard *sh, int32_t k, uint32_t *dst, int64_t cap,
     if (!dst) return PPG_OK;
     if (r > cap) return PPG_BUF_ERROR;
     if (r) HIPCHK(hipMemcpy(dst, sh->recs.p + 4 * sh->h_base[(size_t)k], 16 * (size_t)r, hipMemcpyDeviceToHost));
+    return PPG_OK;
+}
+
+int ppg_shard_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap) {
+    if (!sh || !sh->ran || sh->batches.size() != 1 || !dev_keys) return PPG_ARG_ERROR;
+    if (cap < sh->total_records) return PPG_BUF_ERROR;
+    HIPCHK(hipSetDevice(sh->ctx->device));
+    hipStream_t s = sh->ctx->stream;
+    HIPCHK(ppg_launch_record_keys(s, sh->out.p, sh->jobs.p, sh->res.p, sh->offs.p, sh->oref.p, sh->info.p, sh->base.p,
+                                  sh->recs.p, dev_keys, sh->n));
+    HIPCHK(hipStreamSynchronize(s));
     return PPG_OK;
 }
 

@@ -6,6 +6,8 @@
 //   ppg_parse_serial  the exact Parsing.Parse state machine for chunks the census declines
 //   ppg_scan_counts   exclusive scan of per-chunk record counts -> record bases
 //   ppg_parse_emit    per-record descriptors (n1..n4 newline positions) for fast chunks
+//   ppg_record_keys   per-record spot ("major") number from the identifier line, for pairing
+//                     the two files of a read pair
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "ppg_device.h"
@@ -211,6 +213,48 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_emit(
     }
 }
 
+// Spot number of every record: Identifier = raw[start+1, n1) ("SRR<id>.<major>.<minor> ..."):
+// the digits between its first and second '.'; -1 when the identifier has no such field.  The
+// first record of a chunk that lies wholly inside offset_k is the previous chunk's last record
+// parsed again (the Point fell on a record start) and gets -2, so a pairing can drop
+// it and keep global record numbers aligned.  One block per chunk, a thread per record.
+extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
+    const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
+    const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, const PpgParseInfo *__restrict__ info,
+    const uint64_t *__restrict__ base, const uint32_t *__restrict__ recs, int64_t *__restrict__ keys, int nchunks) {
+    const int k = blockIdx.x;
+    if (k >= nchunks || ires[k].status != 0) return;
+    const uint64_t nrec = info[k].records;
+    const uint8_t *off = offs + oref[k].start;
+    const uint32_t olen = oref[k].len;
+    const uint8_t *body = out + jobs[k].out_off;
+    const uint64_t blen = ires[k].produced;
+    const uint32_t *r = recs + 4 * base[k];
+    int64_t *kk = keys + base[k];
+    for (uint64_t j = threadIdx.x; j < nrec; j += 256) {
+        const uint64_t start = j ? (uint64_t)r[4 * j - 1] + 1 : 0;
+        const uint64_t n1 = r[4 * j];
+        if (j == 0 && (uint64_t)r[3] < olen) { kk[j] = -2; continue; }
+        int64_t key = -1;
+        uint64_t i = start + 1;
+        const uint64_t end = min(n1, start + 96);   // identifiers are short; bound the scan
+        while (i < end && raw_at(off, olen, body, blen, i) != '.') i++;
+        if (i < end) {
+            i++;
+            int64_t v = 0;
+            int nd = 0;
+            uint8_t c = 0;
+            while (i < end && (c = raw_at(off, olen, body, blen, i)) >= '0' && c <= '9' && nd < 18) {
+                v = v * 10 + (c - '0');
+                nd++;
+                i++;
+            }
+            if (nd > 0 && i < end && c == '.') key = v;
+        }
+        kk[j] = key;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Host-side launchers (called from ppg_api.cpp).
 // ------------------------------------------------------------------------------------------
@@ -231,5 +275,14 @@ hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInf
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(ppg_parse_emit, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, n);
     hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, 1);
+    return hipGetLastError();
+}
+
+hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
+                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
+                                  const PpgParseInfo *info, const uint64_t *base, const uint32_t *recs, int64_t *keys,
+                                  int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_record_keys, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, keys, n);
     return hipGetLastError();
 }

@@ -46,18 +46,24 @@ inline int put_u(char *p, uint64_t v) {
 
 inline int digits(uint64_t v) { int n = 1; while (v >= 10) { v /= 10; n++; } return n; }
 
+// mate 0: the reference Generator's single file (major = no/2+1, minor = no%2+1); mate 1/2: one
+// file of a read pair: major = no+1, minor = mate, and the SRR ids are
+// drawn from the record number alone, so R1 and R2 records share them.
+inline uint64_t rec_major(int64_t no, int mate) { return mate ? (uint64_t)no + 1 : (uint64_t)no / 2 + 1; }
+
 // bytes of record `no` (independent of the random draws: ids always have 8 digits)
-inline int64_t rec_size(int64_t no, int L) {
-    uint64_t major = (uint64_t)no / 2 + 1;
+inline int64_t rec_size(int64_t no, int L, int mate = 0) {
+    uint64_t major = rec_major(no, mate);
     int64_t hdr = 1 + 3 + 8 + 1 + digits(major) + 1 + 1 + 1 + digits(major) + 8 + digits((uint64_t)L) + 1;
     return 2 * hdr + 2 * (int64_t)(L + 1);
 }
 
-int64_t write_rec(char *p, uint64_t seed, int64_t no, int L) {
+int64_t write_rec(char *p, uint64_t seed, int64_t no, int L, int mate = 0) {
     uint64_t s = seed * 0xD1B54A32D192ED03ull ^ ((uint64_t)no * 0x9E3779B97F4A7C15ull) ^ 0x5851F42D4C957F2Dull;
     splitmix(s);
+    uint64_t sid = ((uint64_t)no * 0x9E3779B97F4A7C15ull) ^ 0x2545F4914F6CDD1Dull;   // pair-shared ids
     char *p0 = p;
-    uint64_t major = (uint64_t)no / 2 + 1, minor = (uint64_t)no % 2 + 1;
+    uint64_t major = rec_major(no, mate), minor = mate ? (uint64_t)mate : (uint64_t)no % 2 + 1;
     for (int line = 0; line < 2; line++) {
         // header ('@') then, after the sequence, the '+' line with a fresh id (Generator.cs:11-14)
         if (line == 1) {
@@ -71,7 +77,7 @@ int64_t write_rec(char *p, uint64_t seed, int64_t no, int L) {
         }
         *p++ = line == 0 ? '@' : '+';
         memcpy(p, "SRR", 3); p += 3;
-        p += put_u(p, 10000000ull + splitmix(s) % 10000000ull);
+        p += put_u(p, 10000000ull + splitmix(mate ? sid : s) % 10000000ull);
         *p++ = '.'; p += put_u(p, major); *p++ = '.'; p += put_u(p, minor);
         *p++ = ' '; p += put_u(p, major);
         memcpy(p, " length=", 8); p += 8;
@@ -95,22 +101,24 @@ int64_t write_rec(char *p, uint64_t seed, int64_t no, int L) {
 
 extern "C" {
 
-// exact byte size of records [no0, no0+n)
-int64_t ppg_synth_fastq_size(int64_t no0, int64_t n, int read_len) {
+// exact byte size of records [no0, no0+n) of file `mate` (0: single file, 1/2: pair mates)
+int64_t ppg_synth_fastq_size_mate(int64_t no0, int64_t n, int read_len, int mate) {
     int64_t t = 0;
-    for (int64_t no = no0; no < no0 + n; no++) t += rec_size(no, read_len);
+    for (int64_t no = no0; no < no0 + n; no++) t += rec_size(no, read_len, mate);
     return t;
 }
 
-// Writes records [no0, no0+n) into out (cap bytes).  Returns bytes written or -1.
-int64_t ppg_synth_fastq(uint64_t seed, int64_t no0, int64_t n, int read_len, uint8_t *out, int64_t cap,
-                        int threads) {
+int64_t ppg_synth_fastq_size(int64_t no0, int64_t n, int read_len) { return ppg_synth_fastq_size_mate(no0, n, read_len, 0); }
+
+// Writes records [no0, no0+n) of file `mate` into out (cap bytes).  Returns bytes written or -1.
+int64_t ppg_synth_fastq_mate(uint64_t seed, int mate, int64_t no0, int64_t n, int read_len, uint8_t *out,
+                             int64_t cap, int threads) {
     if (threads < 1) threads = 1;
     int64_t per = (n + threads - 1) / threads;
     std::vector<int64_t> off(threads + 1, 0);
     for (int t = 0; t < threads; t++) {
         int64_t a = no0 + std::min(n, t * per), b = no0 + std::min(n, (t + 1) * per);
-        off[t + 1] = off[t] + ppg_synth_fastq_size(a, b - a, read_len);
+        off[t + 1] = off[t] + ppg_synth_fastq_size_mate(a, b - a, read_len, mate);
     }
     if (off[threads] > cap) return -1;
     std::vector<std::thread> th;
@@ -118,11 +126,16 @@ int64_t ppg_synth_fastq(uint64_t seed, int64_t no0, int64_t n, int read_len, uin
         th.emplace_back([=, &off] {
             int64_t a = no0 + std::min(n, t * per), b = no0 + std::min(n, (t + 1) * per);
             char *p = (char *)out + off[t];
-            for (int64_t no = a; no < b; no++) p += write_rec(p, seed, no, read_len);
+            for (int64_t no = a; no < b; no++) p += write_rec(p, seed, no, read_len, mate);
         });
     }
     for (auto &x : th) x.join();
     return off[threads];
+}
+
+int64_t ppg_synth_fastq(uint64_t seed, int64_t no0, int64_t n, int read_len, uint8_t *out, int64_t cap,
+                        int threads) {
+    return ppg_synth_fastq_mate(seed, 0, no0, n, read_len, out, cap, threads);
 }
 
 // Raw-deflates text[lo,hi) primed with dict (dlen<=32768); `last` -> Z_FINISH, else Z_SYNC_FLUSH.

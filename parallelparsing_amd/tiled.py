@@ -16,12 +16,14 @@ from . import Index
 
 
 class TiledFile:
-    def __init__(self, records, repeats, chunksize, read_len=150, seed=0, level=6, piece=4 << 20, threads=16):
+    def __init__(self, records, repeats, chunksize, read_len=150, seed=0, level=6, piece=4 << 20, threads=16,
+                 mate=0):
         S = synth()
         self.records, self.repeats, self.chunksize = records, repeats, chunksize
-        n = S.ppg_synth_fastq_size(0, records, read_len)
+        n = S.ppg_synth_fastq_size_mate(0, records, read_len, mate)
         self.text = np.empty(n, np.uint8)
-        assert S.ppg_synth_fastq(seed, 0, records, read_len, C.c_void_p(self.text.ctypes.data), n, threads) == n
+        assert S.ppg_synth_fastq_mate(seed, mate, 0, records, read_len, C.c_void_p(self.text.ctypes.data), n,
+                                      threads) == n
         cap = n // 2 + (1 << 20)
         seg = np.empty(cap, np.uint8)
         crc = C.c_uint32()
