@@ -53,9 +53,15 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int k
 // which decodes bit-by-bit from count[]/sorted[].  Validity follows zlib 1.2.11 inflate_table:
 // over-subscribed -> error; incomplete -> error unless exactly one code of length 1 (not for
 // the code-length code); no codes at all -> accepted (decoding then fails).  Returns 0 / -1.
+// Per-lane canonical-code description (lane l = code length l, 1..15): number of codes, first
+// code (MSB-first), and index of that length's first symbol in `sorted`.  canon_decode uses it.
+struct Canon {
+    uint32_t count, first, index;
+};
+
 template <int TB>
-__device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t *count_lds, uint16_t *sorted,
-                           int kind, int lane) {
+__device__ int build_table(const uint8_t *lens, int n, uint32_t *table, Canon *canon, uint16_t *sorted, int kind,
+                           int lane) {
     // Runs once per block, so it is written for few registers, not speed: per-length counts,
     // offsets and running ranks live one per lane (lane l holds length l), loops stay rolled.
     uint32_t cnt = 0;
@@ -69,14 +75,15 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t
         }
     }
     int left = 1, maxl = 0;
-    uint32_t offs = 0, run = 0;
+    uint32_t offs = 0, run = 0, first = 0, code = 0;
 #pragma unroll 1
     for (uint32_t l = 1; l < 16; l++) {
         const uint32_t c = rdlane_u(cnt, l);
         left = left * 2 - (int)c;       // stays negative once over-subscribed
         if (c) maxl = (int)l;
-        if ((uint32_t)lane == l) offs = run;
+        if ((uint32_t)lane == l) { offs = run; first = code; }
         run += c;
+        code = (code + c) << 1;         // first code of length l+1 (RFC 1951 3.2.2)
     }
     if (maxl != 0) {
         if (left < 0) return -1;
@@ -101,7 +108,7 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, uint16_t
         }
         if (L) sorted[mypos] = (uint16_t)s;
     }
-    if (count_lds && lane < 16) count_lds[lane] = (uint16_t)(lane == 0 ? 0u : cnt);
+    if (canon) *canon = Canon{lane == 0 || lane > 15 ? 0u : cnt, first, offs};
     __syncthreads();
     for (int e0 = 0; e0 < (1 << TB); e0 += 64) {   // uniform trip count (see ppg_inflate_kernel)
         const int e = e0 + lane;
@@ -134,25 +141,23 @@ __device__ __forceinline__ uint32_t br_take(R &b, uint32_t n) {
     return v;
 }
 
-// Canonical bit-by-bit decode (codes longer than the root table, or invalid patterns).
-// Returns symbol, or -1 for an invalid code.  Needs bn >= 15.
+// Canonical decode of the next code, all 15 lengths at once: lane l reverses the next l bits
+// (DEFLATE codes are MSB-first in an LSB-first stream) and tests them against the range of codes
+// of length l.  For a prefix code exactly one length matches; ballot + ff1 finds it.  Returns the
+// symbol and consumes the code, or -1 (no code matches: invalid).  Needs bn >= 15.
 template <class R>
-__device__ int slow_decode(R &b, const uint16_t *count, const uint16_t *sorted) {
-    uint32_t code = 0, first = 0, index = 0;
-    for (uint32_t l = 1; l < 16; l++) {
-        code |= (uint32_t)(b.bb >> (l - 1)) & 1u;
-        uint32_t c = uni(count[l]);
-        if (code - first < c) {
-            uint32_t sym = uni(sorted[index + code - first]);
-            b.bb >>= l;
-            b.bn -= l;
-            return (int)sym;
-        }
-        index += c;
-        first = (first + c) << 1;
-        code <<= 1;
-    }
-    return -1;
+__device__ __forceinline__ int canon_decode(R &b, const Canon &c, const uint16_t *sorted, int lane) {
+    const uint32_t bits = __builtin_bitreverse32((uint32_t)b.bb);   // next bit in the MSB
+    const uint32_t l = (uint32_t)lane;
+    const uint32_t code = (l >= 1 && l <= 15) ? bits >> (32 - l) : 0u;
+    const uint64_t hit = __ballot(l >= 1 && l <= 15 && code - c.first < c.count);
+    if (!hit) return -1;
+    const uint32_t L = (uint32_t)__builtin_ctzll(hit);
+    const uint32_t idx = rdlane_u(c.index + code - c.first, L);
+    const int sym = (int)__builtin_amdgcn_readfirstlane(sorted[idx]);
+    b.bb >>= L;
+    b.bn -= L;
+    return sym;
 }
 
 // status codes (ZResult, Interop/Conventions.cs:9-20)

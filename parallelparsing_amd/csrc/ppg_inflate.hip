@@ -42,8 +42,6 @@ struct __attribute__((aligned(16))) InflateLds {
         uint16_t cl_sorted[20];
     };
     uint16_t dst_sorted[32];
-    uint16_t lit_count[16];
-    uint16_t dst_count[16];
     uint8_t lens[320];
 };
 
@@ -285,6 +283,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     uint32_t fl_done = 0;                                    // flushed up to this position
     uint32_t fl_next = UNIT - (uint32_t)(out_off & (UNIT - 1));   // next global 4 KiB boundary
     int status = ST_OK, flags = 0, last = 0, in_block = 0;
+    Canon clit = {0, 0, 0}, cdst = {0, 0, 0};   // per-lane canonical codes of the current block
 
     while (pos < len && !last) {
         r.sg = uni(r.sg);
@@ -339,8 +338,8 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 S.lens[s] = L;
             }
             __syncthreads();
-            build_table<LBT>(S.lens, 288, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane);
-            build_table<DB>(S.lens + 288, 32, S.dst, S.dst_count, S.dst_sorted, TAB_DST, lane);
+            build_table<LBT>(S.lens, 288, S.lit, &clit, S.lit_sorted, TAB_LIT, lane);
+            build_table<DB>(S.lens + 288, 32, S.dst, &cdst, S.dst_sorted, TAB_DST, lane);
         } else {
             // ---- dynamic Huffman codes (RFC 1951 3.2.7) ----
             rd_refill(r, S.stream, lane);
@@ -381,8 +380,8 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             __syncthreads();
             if (bad) { status = ST_DATA_ERROR; break; }
             if (uni(S.lens[256]) == 0) { status = ST_DATA_ERROR; break; }   // no end-of-block code
-            if (build_table<LBT>(S.lens, (int)hlit, S.lit, S.lit_count, S.lit_sorted, TAB_LIT, lane) != 0) { status = ST_DATA_ERROR; break; }
-            if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, S.dst_count, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
+            if (build_table<LBT>(S.lens, (int)hlit, S.lit, &clit, S.lit_sorted, TAB_LIT, lane) != 0) { status = ST_DATA_ERROR; break; }
+            if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, &cdst, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
         }
         in_block = 1;
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
@@ -507,7 +506,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
             rd_seek(r, S.stream, bp, lane);
             rd_refill(r, S.stream, lane);
-            const int sym = slow_decode(r, S.lit_count, S.lit_sorted);
+            const int sym = canon_decode(r, clit, S.lit_sorted, lane);
             if (sym < 0 || sym >= 286) { status = ST_DATA_ERROR; break; }
             if (sym < 256) {
                 if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)sym;
@@ -519,7 +518,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             } else {
                 const uint32_t ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
                 rd_refill(r, S.stream, lane);
-                const int dsym = slow_decode(r, S.dst_count, S.dst_sorted);
+                const int dsym = canon_decode(r, cdst, S.dst_sorted, lane);
                 if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
                 const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
                 const uint32_t n = min(ml, len - pos);
@@ -547,7 +546,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     }
     if (status == ST_OK && in_block && pos == len) {
         rd_refill(r, S.stream, lane);
-        if (slow_decode(r, S.lit_count, S.lit_sorted) == 256) end_bit = rd_pos(r);
+        if (canon_decode(r, clit, S.lit_sorted, lane) == 256) end_bit = rd_pos(r);
         else flags |= PPG_FLAG_NO_EOB;
     }
     if (lane == 0) {
