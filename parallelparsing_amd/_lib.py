@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libppgpu.so")
+LIB_PATH = os.environ.get("PPG_LIB_PATH") or os.path.join(_HERE, "libppgpu.so")
 SYNTH_PATH = os.path.join(_HERE, "libppgsynth.so")
 
 PPG_OK = 0
