@@ -38,6 +38,7 @@ extern "C" {
 #define PPG_INDEX_OUT_OF_RANGE (-50) /* C# IndexOutOfRangeException (>32 KiB without '@') */
 #define PPG_IO_ERROR (-51)
 #define PPG_ARG_ERROR (-52)
+#define PPG_UNSUPPORTED (-53)        /* input the GPU CreateIndex does not take (not single-member gzip) */
 #define PPG_DEVICE_ERROR (-100)
 #define PPG_NO_DEVICE (-101)
 
@@ -45,12 +46,29 @@ extern "C" {
 #define PPG_CHUNK 16384   /* Common/Constants.cs:12 */
 
 /* ======================= Index (Common/Index.cs, Common/IndexIO.cs) ======================= */
+typedef struct ppg_ctx ppg_ctx;       /* one GPU (see "device context" below) */
 typedef struct ppg_index ppg_index;
 
 /* CreateIndex: Core.BuildDeflateIndex(FileStream, uint chunksize) — Decompressor/Core.cs:14-131.
  * Host-side (serial zlib pass, as in the reference).  _mem takes the whole .gz in memory. */
 int ppg_index_build_file(const char *gz_path, uint32_t chunksize, ppg_index **out);
 int ppg_index_build_mem(const uint8_t *gz, int64_t gz_len, uint32_t chunksize, ppg_index **out);
+
+/* CreateIndex on the GPU: the same Points as ppg_index_build_* (Core.BuildDeflateIndex,
+ * Decompressor/Core.cs:14-131) from a block-parallel decode (ppg_index_gpu.cpp): candidate block
+ * headers per piece of piece_bytes (0: automatic), a verified chain of block ends, exact output
+ * per piece, then the '@' census.  gz: the whole single-member .gz, in host memory or (gz_on_device,
+ * 4-byte aligned) in device memory.  out_capacity bounds the exact-output buffer (0: free HBM).
+ * Returns PPG_UNSUPPORTED for zlib-wrapped / multi-member input (use ppg_index_build_file). */
+int ppg_index_build_gpu(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
+                        int64_t piece_bytes, int64_t out_capacity, ppg_index **out);
+int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksize, int64_t piece_bytes,
+                             ppg_index **out);
+/* Last GPU CreateIndex on ctx: [0] finder ms, [1] pass-1 ms, [2] chain check ms, [3] pass-2 ms,
+ * [4] census + windows ms, [5] total ms, [6] pieces, [7] real pieces, [8] pass-1 redos,
+ * [9] pass-2 redos, [10] pass-2 rounds, [11] blocks, [12] points, [13] output bytes,
+ * [14] file upload ms (ppg_index_build_gpu_file). */
+int ppg_index_build_gpu_stats(ppg_ctx *ctx, double *vals, int32_t n);
 
 /* Serialize / Deserialize — Common/IndexIO.cs:7-27 / :29-53 (byte-identical .gzi format). */
 int ppg_index_serialize(const ppg_index *ix, const char *path);
@@ -72,7 +90,6 @@ const uint8_t *ppg_index_offset(const ppg_index *ix, int32_t i);  /* Point.offse
 void ppg_index_free(ppg_index *ix);
 
 /* ================================= device context ================================= */
-typedef struct ppg_ctx ppg_ctx;
 
 int ppg_device_count(int *n);
 int ppg_open(int device, ppg_ctx **out);

@@ -237,6 +237,38 @@ class Core:
         return Index(h.value)
 
     @staticmethod
+    def BuildDeflateIndexGpu(gz, chunksize, device=None, piece_bytes=0, out_capacity=0):
+        """CreateIndex on the GPU (ppg_index_gpu.cpp): the same Points as BuildDeflateIndex for a
+        single-member gzip, from a block-parallel decode.  gz: a path, bytes / uint8 array (host),
+        or a uint8 torch tensor on the device.  Raises PpgError(PPG_UNSUPPORTED) for zlib-wrapped
+        or multi-member input (BuildDeflateIndex handles those)."""
+        dev = device or Device.default()
+        h = C.c_void_p()
+        cs = int(chunksize) & 0xFFFFFFFF
+        if isinstance(gz, (str, os.PathLike)):
+            rc = lib.ppg_index_build_gpu_file(dev.handle, os.fsencode(gz), cs, int(piece_bytes), C.byref(h))
+        elif hasattr(gz, "data_ptr"):
+            rc = lib.ppg_index_build_gpu(dev.handle, C.c_void_p(gz.data_ptr()), gz.numel(), 1, cs, int(piece_bytes),
+                                         int(out_capacity), C.byref(h))
+        else:
+            a = _as_u8(gz)
+            rc = lib.ppg_index_build_gpu(dev.handle, _ptr(a), a.size, 0, cs, int(piece_bytes), int(out_capacity),
+                                         C.byref(h))
+        check(rc, "Core.BuildDeflateIndexGpu")
+        return Index(h.value)
+
+    GPU_INDEX_STATS = ("finder_ms", "pass1_ms", "chain_ms", "pass2_ms", "census_ms", "total_ms", "pieces",
+                       "real_pieces", "redo1", "redo2", "rounds2", "blocks", "points", "output_bytes", "upload_ms")
+
+    @staticmethod
+    def gpu_index_stats(device=None):
+        """Timings and counts of the last BuildDeflateIndexGpu on a device (ppg_index_build_gpu_stats)."""
+        dev = device or Device.default()
+        v = (C.c_double * 16)()
+        check(lib.ppg_index_build_gpu_stats(dev.handle, v, 16), "ppg_index_build_gpu_stats")
+        return dict(zip(Core.GPU_INDEX_STATS, list(v)))
+
+    @staticmethod
     def ExtractDeflateIndex(file_buffer, index, k, buf=None, device=None, with_records=False):
         """Decompress checkpoint k (Core.cs:133-192) on the GPU.  file_buffer = file bytes
         [Index[k].Input-1, Index[k+1].Input-1].  Returns the produced byte count written into buf

@@ -17,13 +17,14 @@ PPG_BUF_ERROR = -5
 PPG_INDEX_OUT_OF_RANGE = -50
 PPG_IO_ERROR = -51
 PPG_ARG_ERROR = -52
+PPG_UNSUPPORTED = -53
 PPG_DEVICE_ERROR = -100
 PPG_NO_DEVICE = -101
 
 # ZResult names (Interop/Conventions.cs:9-20) for messages
 _NAMES = {0: "OK", 1: "STREAM_END", 2: "NEED_DICT", -1: "ERRNO", -2: "STREAM_ERROR", -3: "DATA_ERROR",
           -4: "MEM_ERROR", -5: "BUF_ERROR", -6: "VERSION_ERROR", -50: "INDEX_OUT_OF_RANGE", -51: "IO_ERROR",
-          -52: "ARG_ERROR", -100: "DEVICE_ERROR", -101: "NO_DEVICE"}
+          -52: "ARG_ERROR", -53: "UNSUPPORTED", -100: "DEVICE_ERROR", -101: "NO_DEVICE"}
 
 
 class PpgError(RuntimeError):
@@ -64,6 +65,9 @@ P = C.POINTER
 _SIGS = {
     "ppg_index_build_file": (C.c_int, [C.c_char_p, u32, P(vp)]),
     "ppg_index_build_mem": (C.c_int, [vp, i64, u32, P(vp)]),
+    "ppg_index_build_gpu": (C.c_int, [vp, vp, i64, C.c_int, u32, i64, i64, P(vp)]),
+    "ppg_index_build_gpu_file": (C.c_int, [vp, C.c_char_p, u32, i64, P(vp)]),
+    "ppg_index_build_gpu_stats": (C.c_int, [vp, P(C.c_double), i32]),
     "ppg_index_serialize": (C.c_int, [vp, C.c_char_p]),
     "ppg_index_deserialize": (C.c_int, [C.c_char_p, P(vp)]),
     "ppg_index_from_points": (C.c_int, [i32, vp, vp, vp, vp, vp, vp, i32, P(vp)]),

@@ -10,6 +10,11 @@ struct PpgInflateJob {
     uint64_t out_len;     // to.Output - from.Output (Core.cs:140)
     uint64_t dict_off;    // byte offset of from.Window (32 KiB) in the dictionary buffer
     uint64_t expect_end;  // 8*to.Input - to.Bits (R-E5), or ~0 when not checkable (last chunk)
+    // CreateIndex pass 1 only (ppg_inflate_kernel<.., IX = true>): decode whole blocks until one
+    // ends at or past stop_bit (or the final block ends); block ends go to blk[blk_off, +blk_cap)
+    uint64_t stop_bit;
+    uint32_t blk_off;
+    uint32_t blk_cap;
 };
 
 struct PpgInflateResult {
@@ -17,6 +22,22 @@ struct PpgInflateResult {
     uint64_t end_bit;     // bit position after the chunk's trailing end-of-block code
     int32_t status;       // 0 or a ZResult error code (Interop/Conventions.cs:9-20)
     int32_t flags;        // PPG_FLAG_*
+    uint32_t nblocks;     // CreateIndex pass 1: block ends recorded
+    uint32_t last;        // CreateIndex pass 1: the final block (BFINAL) was decoded
+};
+
+// CreateIndex: one deflate block end (Core.cs:98 -- where inflate(Z_BLOCK) reports data_type & 128)
+struct PpgBlockEnd {
+    uint64_t end_bit;     // absolute bit position after the block (the next block's header)
+    uint64_t out_end;     // output bytes of the piece up to the block end
+};
+
+// CreateIndex: '@' census of one block's output (Core.cs:79-96), positions relative to the block
+struct PpgAtStats {
+    uint32_t count;       // '@' bytes
+    int32_t first;        // first '@' (-1: none)
+    int32_t last;         // last '@' (-1: none)
+    uint32_t max_gap;     // largest distance between consecutive '@' inside the block
 };
 
 // offset_k bytes (Common/Index.cs:75) live concatenated in one device buffer
@@ -32,5 +53,19 @@ struct PpgParseInfo {
     uint32_t serial;      // 1: parsed by the exact serial state machine
 };
 
+// CreateIndex: a 32 KiB history ending at output position `end` of a piece (ppg_gather_kernel)
+struct PpgGather {
+    uint64_t out_off;     // position p >= 0 of the piece is out[out_off + (p & mask)]
+    uint64_t dict_off;    // position p < 0 is dicts[dict_off + 32768 + p]
+    uint64_t end;
+    uint64_t mask;        // 0xFFFF for pass-1 rings, ~0 for plain output
+    uint64_t ref_off;     // with a reference buffer: compare against ref[ref_off, +32768)
+};
+
+struct PpgSpan {          // byte range [lo, hi) of an output buffer
+    uint64_t lo, hi;
+};
+
 #define PPG_FLAG_NO_EOB 1     // the symbol after the last output byte is not end-of-block
 #define PPG_FLAG_OVERRUN 2    // decoding consumed bits past the chunk's compressed slice
+#define PPG_FLAG_BLK_FULL 16  // CreateIndex pass 1: more block ends than blk_cap

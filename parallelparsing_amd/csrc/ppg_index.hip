@@ -1,0 +1,270 @@
+// ppg_index.hip — gfx950 kernels of the GPU CreateIndex (host side: ppg_index_gpu.cpp).
+//
+// Core.BuildDeflateIndex (Decompressor/Core.cs:14-131) is one serial zlib pass over the whole
+// member.  On the GPU the member is cut into pieces that are decoded in parallel
+// (ppg_inflate_kernel<.., IX = true>); these kernels supply the pieces' starting points, the
+// 32 KiB histories that chain them, and the '@' census from which the Points are chosen:
+//   ppg_block_find_kernel   first plausible dynamic-block header at or after each piece's nominal
+//                           start (one wave per piece; lanes test 64 bit offsets at a time)
+//   ppg_gather_kernel       32 KiB histories ending at a given output position (piece tails,
+//                           Point windows), optionally compared against a previous copy
+//   ppg_at_stats_kernel     per-block '@' count / first / last / largest gap (Core.cs:79-96)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "ppg_device.h"
+#include "ppg_huffman.h"
+
+namespace {
+
+// wave-uniform bit reader straight from global memory (the finder's header check)
+struct GBits {
+    const uint32_t *w;
+    uint64_t nw;
+    uint64_t pos;
+    __device__ uint32_t peek() const {
+        const uint64_t i = pos >> 5;
+        const uint32_t x0 = i < nw ? w[i] : 0u, x1 = i + 1 < nw ? w[i + 1] : 0u;
+        return __builtin_amdgcn_alignbit(x1, x0, (uint32_t)(pos & 31));
+    }
+    __device__ uint32_t take(uint32_t n) {
+        const uint32_t v = peek() & ((1u << n) - 1u);
+        pos += n;
+        return v;
+    }
+};
+
+struct FindLds {
+    uint8_t lens[320];
+    uint32_t cl[1 << CB];
+    uint32_t scratch[64];
+    uint16_t sorted[288];
+};
+
+// Would zlib 1.2.11 accept a dynamic-block header at bit c?  (inflate.c TABLE/LENLENS/CODELENS:
+// HLIT/HDIST ranges, complete code-length code, repeat rules, litlen/distance codes per
+// inflate_table, end-of-block present.)  Every true block header passes; false positives are
+// caught by the pass-1 chain check.
+__device__ bool header_ok(const uint32_t *comp, uint64_t nwords, uint64_t c, FindLds &S, int lane) {
+    GBits g{comp, nwords, c + 3};
+    const uint32_t hlit = g.take(5) + 257, hdist = g.take(5) + 1, hclen = g.take(4) + 4;
+    if (hlit > 286 || hdist > 30) return false;
+    {
+        GBits f{comp, nwords, g.pos + 3ull * (uint32_t)(lane < 19 ? lane : 0)};
+        const uint32_t v = f.take(3);
+        __syncthreads();
+        if (lane < 19) S.lens[c_clorder[lane]] = (uint8_t)((uint32_t)lane < hclen ? v : 0u);
+        __syncthreads();
+    }
+    g.pos += 3ull * hclen;
+    if (build_table<CB>(S.lens, 19, S.cl, nullptr, S.sorted, TAB_CL, lane) != 0) return false;
+    uint32_t idx = 0;
+    const uint32_t total = hlit + hdist;
+    while (idx < total) {
+        const uint32_t e = uni(S.cl[g.peek() & ((1u << CB) - 1)]);
+        const uint32_t L = e & 15;
+        if (L == 0) return false;
+        g.pos += L;
+        const uint32_t sym = e >> 8;
+        uint32_t val = 0, rep = 1;
+        if (sym < 16) {
+            val = sym;
+        } else if (sym == 16) {
+            if (idx == 0) return false;
+            val = uni(S.lens[idx - 1]);
+            rep = 3 + g.take(2);
+        } else if (sym == 17) {
+            rep = 3 + g.take(3);
+        } else {
+            rep = 11 + g.take(7);
+        }
+        if (idx + rep > total) return false;
+        for (uint32_t j0 = 0; j0 < rep; j0 += 64)
+            if (j0 + lane < rep) S.lens[idx + j0 + lane] = (uint8_t)val;
+        idx += rep;
+        __syncthreads();
+    }
+    if (uni(S.lens[256]) == 0) return false;
+    // validity only (build_table's checks); the 64-entry table is scratch
+    if (build_table<6>(S.lens, (int)hlit, S.scratch, nullptr, S.sorted, TAB_LIT, lane) != 0) return false;
+    if (build_table<6>(S.lens + hlit, (int)hdist, S.scratch, nullptr, S.sorted, TAB_DST, lane) != 0) return false;
+    return true;
+}
+
+}  // namespace
+
+// cand[k] = the first bit b in [lo[k], hi[k]) where a dynamic Huffman block header zlib would
+// accept starts, or ~0.  Prefilter per lane: BTYPE = 2, HLIT <= 29, HDIST <= 29 and a complete
+// code-length code (Kraft sum exactly 1); survivors get the full header_ok check, lowest first.
+__global__ __launch_bounds__(64) void ppg_block_find_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
+                                                            const uint64_t *__restrict__ lo,
+                                                            const uint64_t *__restrict__ hi, uint64_t *cand, int n) {
+    __shared__ FindLds S;
+    const int k = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (k >= n) return;
+    const uint64_t a = lo[k], b = hi[k];
+    uint64_t found = ~0ull;
+    for (uint64_t base = a; base < b; base += 64) {
+        const uint64_t bit = base + (uint64_t)lane;
+        const uint64_t w = bit >> 5;
+        const uint32_t sh = (uint32_t)(bit & 31);
+        const uint32_t x0 = w < nwords ? comp[w] : 0u, x1 = w + 1 < nwords ? comp[w + 1] : 0u;
+        const uint32_t x2 = w + 2 < nwords ? comp[w + 2] : 0u, x3 = w + 3 < nwords ? comp[w + 3] : 0u;
+        const uint32_t v0 = __builtin_amdgcn_alignbit(x1, x0, sh);
+        const uint32_t v1 = __builtin_amdgcn_alignbit(x2, x1, sh);
+        const uint32_t v2 = __builtin_amdgcn_alignbit(x3, x2, sh);
+        const uint64_t u01 = ((uint64_t)v1 << 32) | v0, u12 = ((uint64_t)v2 << 32) | v1;
+        bool ok = bit < b && ((v0 >> 1) & 3) == 2 && ((v0 >> 3) & 31) <= 29 && ((v0 >> 8) & 31) <= 29;
+        const uint32_t ncl = ((v0 >> 13) & 15) + 4;
+        uint32_t kraft = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 19; i++) {
+            const uint32_t o = 17 + 3 * i;
+            const uint32_t L = (uint32_t)((o + 3 <= 64 ? (u01 >> o) : (u12 >> (o - 32))) & 7u);
+            kraft += (i < ncl && L) ? (128u >> L) : 0u;
+        }
+        ok = ok && kraft == 128;
+        uint64_t m = __ballot(ok);
+        while (m) {
+            const uint32_t c = (uint32_t)__builtin_ctzll(m);
+            if (header_ok(comp, nwords, base + c, S, lane)) {
+                found = base + c;
+                break;
+            }
+            m &= m - 1;
+        }
+        if (found != ~0ull) break;
+    }
+    if (lane == 0) cand[k] = found;
+}
+
+// dst[k] = the 32 KiB of history before output position g[k].end of a piece: position p >= 0 is
+// out[out_off + (p & mask)] (mask: 64 KiB rings of pass 1, or ~0), p < 0 is
+// dicts[dict_off + 32768 + p] (the piece's own starting history).  With ref, diff[k] = 1 when
+// the new history differs from ref[ref_off, +32768).
+__global__ __launch_bounds__(256) void ppg_gather_kernel(const uint8_t *__restrict__ out,
+                                                         const uint8_t *__restrict__ dicts,
+                                                         const PpgGather *__restrict__ g, uint8_t *__restrict__ dst,
+                                                         const uint8_t *__restrict__ ref, uint32_t *diff, int n) {
+    const int k = blockIdx.x;
+    if (k >= n) return;
+    const PpgGather G = g[k];
+    uint32_t *d32 = (uint32_t *)(dst + (uint64_t)k * 32768);
+    const uint32_t *r32 = ref ? (const uint32_t *)(ref + G.ref_off) : nullptr;
+    int differs = 0;
+    for (uint32_t i = threadIdx.x; i < 8192; i += 256) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int64_t p = (int64_t)G.end - 32768 + 4 * (int64_t)i + q;
+            const uint32_t byte = p >= 0 ? out[G.out_off + ((uint64_t)p & G.mask)] : dicts[G.dict_off + 32768 + p];
+            v |= byte << (8 * q);
+        }
+        d32[i] = v;
+        if (r32 && r32[i] != v) differs = 1;
+    }
+    differs = __syncthreads_or(differs);
+    if (diff && threadIdx.x == 0) diff[k] = (uint32_t)differs;
+}
+
+// '@' census of out[s.lo, s.hi) per block (Core.cs:79-96): count, first and last '@' (relative to
+// lo) and the largest distance between consecutive '@' inside the block (SURVEY Q4 needs the
+// gaps).  One wave per block, 16 bytes per lane per step.
+__global__ __launch_bounds__(64) void ppg_at_stats_kernel(const uint8_t *__restrict__ out,
+                                                          const PpgSpan *__restrict__ spans, PpgAtStats *st, int n) {
+    const int k = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (k >= n) return;
+    const uint64_t a = spans[k].lo, b = spans[k].hi;
+    uint32_t cnt = 0, gmax = 0;
+    int32_t first = 0x7FFFFFFF, carry = -1;   // carry: last '@' so far (relative), -1 none
+    for (uint64_t g0 = a & ~15ull; g0 < b; g0 += 1024) {
+        const uint64_t q = g0 + 16ull * (uint64_t)lane;
+        uint32_t m = 0;
+        if (q < b) {
+            const uint4 v = *(const uint4 *)(out + q);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t x = w[j] ^ 0x40404040u;   // '@' bytes -> 0
+                const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+                m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * j);
+            }
+            // bytes outside [a, b)
+            if (q < a) m &= 0xFFFFu << (uint32_t)(a - q);
+            if (q + 16 > b) m &= (1u << (uint32_t)(b - q)) - 1u;
+        }
+        const int32_t rel = (int32_t)(q - a);
+        const int32_t f = m ? rel + __builtin_ctz(m) : 0x7FFFFFFF;
+        const int32_t l = m ? rel + 31 - __builtin_clz(m) : -1;
+        // gaps between consecutive '@' of this lane's 16 bytes
+        uint32_t mm = m, lg = 0;
+        int32_t prev = -1;
+        while (mm) {
+            const int32_t i = __builtin_ctz(mm);
+            if (prev >= 0) lg = max(lg, (uint32_t)(i - prev));
+            prev = i;
+            mm &= mm - 1;
+        }
+        // last '@' before this lane's bytes: prefix max over lower lanes, then the carry
+        int32_t incl = l;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t y = __shfl_up(incl, d);
+            if (lane >= d) incl = max(incl, y);
+        }
+        int32_t excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = -1;
+        excl = max(excl, carry);
+        if (m && excl >= 0) lg = max(lg, (uint32_t)(f - excl));
+        gmax = max(gmax, lg);
+        carry = max(carry, __shfl(incl, 63));
+        cnt += (uint32_t)__builtin_popcount(m);
+        first = min(first, f);
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        cnt += __shfl_xor(cnt, d);
+        gmax = max(gmax, (uint32_t)__shfl_xor((int)gmax, d));
+        first = min(first, __shfl_xor(first, d));
+    }
+    if (lane == 0) st[k] = PpgAtStats{cnt, first == 0x7FFFFFFF ? -1 : first, carry, gmax};
+}
+
+// dense[pre[k] + i] = blk[jobs[k].blk_off + i] for i < min(res[k].nblocks, blk_cap): pass-1 block
+// lists packed for one device-to-host copy
+__global__ __launch_bounds__(256) void ppg_pack_blocks_kernel(const PpgBlockEnd *__restrict__ blk,
+                                                              const PpgInflateJob *__restrict__ jobs,
+                                                              const PpgInflateResult *__restrict__ res,
+                                                              const uint64_t *__restrict__ pre, PpgBlockEnd *dense, int n) {
+    const int k = blockIdx.x;
+    if (k >= n) return;
+    const uint32_t nb = min(res[k].nblocks, jobs[k].blk_cap);
+    for (uint32_t i = threadIdx.x; i < nb; i += 256) dense[pre[k] + i] = blk[jobs[k].blk_off + i];
+}
+
+hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const PpgInflateJob *jobs,
+                                  const PpgInflateResult *res, const uint64_t *pre, PpgBlockEnd *dense, int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_pack_blocks_kernel, dim3(n), dim3(256), 0, s, blk, jobs, res, pre, dense, n);
+    return hipGetLastError();
+}
+
+hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
+                                 const uint64_t *hi, uint64_t *cand, int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_block_find_kernel, dim3(n), dim3(64), 0, s, comp, nwords, lo, hi, cand, n);
+    return hipGetLastError();
+}
+
+hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
+                             const uint8_t *ref, uint32_t *diff, int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_gather_kernel, dim3(n), dim3(256), 0, s, out, dicts, g, dst, ref, diff, n);
+    return hipGetLastError();
+}
+
+hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan *spans, PpgAtStats *st, int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_at_stats_kernel, dim3(n), dim3(64), 0, s, out, spans, st, n);
+    return hipGetLastError();
+}

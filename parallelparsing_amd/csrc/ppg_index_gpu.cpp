@@ -1,0 +1,621 @@
+// ppg_index_gpu.cpp — CreateIndex on the GPU: the same Points as Core.BuildDeflateIndex
+// (Decompressor/Core.cs:14-131; the host restatement is IndexBuilder in ppg_api.cpp).
+//
+// The reference makes one serial zlib inflate(Z_BLOCK) pass over the member, counting '@' bytes
+// and dropping a Point at the first block end after more than chunksize-8 of them.  The Points
+// depend only on (a) where the deflate blocks end, (b) how many '@' each block emits, (c) the
+// 32 KiB of output before each chosen block end.  All three come out of a block-parallel decode:
+//
+//   1. finder     the compressed member is cut into pieces of piece_bytes; one wave per piece
+//                 finds the first bit where a dynamic-block header zlib would accept starts
+//                 (ppg_block_find_kernel).  Piece 0 starts right after the gzip header.
+//   2. pass 1     every piece decodes whole blocks from its candidate with an all-zero history
+//                 until a block ends at or past the next piece's candidate, recording each block
+//                 end (ppg_inflate_kernel IX).  Block boundaries do not depend on history bytes,
+//                 so walking the pieces in order proves each start: piece j+1 is real iff the
+//                 (real) piece j ended exactly there; otherwise piece j+1 is redone from where
+//                 piece j really ended.  Each piece leaves its last 32 KiB (its "tail").
+//   3. pass 2     every piece is decoded again (the DecompressAll kernel) with the previous
+//                 piece's pass-1 tail as history.  Piece 0's history is exact (none), so by
+//                 induction piece j is exact iff the tail it was given equals the tail piece j-1
+//                 now produces; pieces whose history changed are redone until nothing changes.
+//                 In practice pass-1 tails are already exact (a piece's last 32 KiB essentially
+//                 never copies from its own starting history), so pass 2 runs once.
+//   4. census     per-block '@' statistics over the exact output (ppg_at_stats_kernel); the host
+//                 walks the blocks in order exactly as Core.cs:98-110 does and gathers the 32 KiB
+//                 windows of the chosen Points on the GPU (ppg_gather_kernel).
+//
+// Scope: single-member gzip (the reference's input).  A zlib-wrapped stream, a
+// multi-member file or trailing bytes return PPG_UNSUPPORTED (ppg_index_build_file handles them).
+// The trailer's ISIZE is checked; its CRC-32 is not (zlib would also reject a bad CRC).
+#include "ppg_host.h"
+#include <chrono>
+#include <memory>
+#include <fcntl.h>
+#include <unistd.h>
+
+hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
+                              const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
+                              int njobs);
+hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
+                                 const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
+                                 int njobs);
+hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
+                                 const uint64_t *hi, uint64_t *cand, int n);
+hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
+                             const uint8_t *ref, uint32_t *diff, int n);
+hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan *spans, PpgAtStats *st, int n);
+hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const PpgInflateJob *jobs,
+                                  const PpgInflateResult *res, const uint64_t *pre, PpgBlockEnd *dense, int n);
+
+namespace {
+
+constexpr uint64_t kRing = 65536;       // pass-1 output ring per piece (IX_RING_BYTES)
+constexpr int64_t kMaxRun = kWin;       // at most 32768 bytes since the last '@'
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// RFC 1952 member header length, or -1 (not a gzip member this path handles)
+int64_t gzip_header_len(const uint8_t *h, int64_t n) {
+    if (n < 10 || h[0] != 31 || h[1] != 139 || h[2] != 8) return -1;
+    const int flg = h[3];
+    if (flg & 0xE0) return -1;
+    int64_t p = 10;
+    if (flg & 4) {                      // FEXTRA
+        if (p + 2 > n) return -1;
+        p += 2 + (int64_t)(h[p] | (h[p + 1] << 8));
+    }
+    for (int f : {8, 16}) {             // FNAME, FCOMMENT: zero-terminated
+        if (!(flg & f)) continue;
+        while (p < n && h[p]) p++;
+        if (p >= n) return -1;
+        p++;
+    }
+    if (flg & 2) p += 2;                // FHCRC
+    return p <= n ? p : -1;
+}
+
+struct Piece {
+    uint32_t slot;                      // pass-1 job / ring / tail slot
+    uint64_t start;                     // absolute bit of the piece's first block header
+};
+
+struct Builder {
+    ppg_ctx *ctx;
+    hipStream_t s;
+    const uint32_t *comp;
+    uint64_t nwords;
+    int64_t len;
+    uint32_t chunksize;
+    double *stat;                       // ctx->ix_stats
+
+    // pass 1
+    std::vector<PpgInflateJob> hjobs;
+    std::vector<PpgInflateResult> hres;
+    std::vector<PpgBlockEnd> hblk;
+    DevBuf<PpgInflateJob> jobs;
+    DevBuf<PpgInflateResult> res;
+    DevBuf<PpgBlockEnd> blk, bigblk;
+    DevBuf<uint8_t> ring;
+    DevBuf<uint8_t> tails;              // slot 0: zeros; slot q + 1: tail of pass-1 job q
+    DevBuf<PpgGather> gat;
+    DevBuf<uint32_t> diff;
+    DevBuf<uint64_t> dpre;
+    DevBuf<PpgBlockEnd> dense;
+
+    uint8_t *tail_slot(uint32_t q) { return tails.p + (uint64_t)(q + 1) * kWin; }
+
+    // pass-1 decode of job slots `which` (ascending); refreshes their results, blocks and tails
+    int run_pass1(const std::vector<uint32_t> &which, bool big) {
+        if (which.empty()) return PPG_OK;
+        // contiguous runs launch as one grid; the common case is all slots at once
+        for (size_t i = 0; i < which.size();) {
+            size_t e = i + 1;
+            while (e < which.size() && which[e] == which[e - 1] + 1 && !big) e++;
+            const uint32_t q0 = which[i], n = (uint32_t)(e - i);
+            HIPCHK(hipMemcpyAsync(jobs.p + q0, hjobs.data() + q0, sizeof(PpgInflateJob) * n, hipMemcpyHostToDevice, s));
+            HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jobs.p + q0, tails.p, ring.p, res.p + q0,
+                                         big ? bigblk.p : blk.p, (int)n));
+            HIPCHK(hipMemcpyAsync(hres.data() + q0, res.p + q0, sizeof(PpgInflateResult) * n, hipMemcpyDeviceToHost, s));
+            i = e;
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        // tails and block lists
+        std::vector<PpgGather> g(which.size());
+        for (size_t i = 0; i < which.size(); i++) {
+            const uint32_t q = which[i];
+            g[i] = PpgGather{(uint64_t)q * kRing, 0, hres[q].produced, kRing - 1, 0};
+        }
+        HIPCHK(gat.alloc(g.size()));
+        HIPCHK(hipMemcpyAsync(gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
+        for (size_t i = 0; i < which.size();) {     // one gather per contiguous run (dst = tail slots)
+            size_t e = i + 1;
+            while (e < which.size() && which[e] == which[e - 1] + 1) e++;
+            HIPCHK(ppg_launch_gather(s, ring.p, tails.p, gat.p + i, tail_slot(which[i]), nullptr, nullptr, (int)(e - i)));
+            i = e;
+        }
+        if (big) {
+            const uint32_t q = which[0];
+            const uint32_t nb = std::min(hres[q].nblocks, hjobs[q].blk_cap);
+            hblk_big.assign(nb, PpgBlockEnd{0, 0});
+            if (nb) HIPCHK(hipMemcpyAsync(hblk_big.data(), bigblk.p, sizeof(PpgBlockEnd) * nb, hipMemcpyDeviceToHost, s));
+        } else {
+            // pack the runs' block lists densely on the device, one copy back
+            std::vector<uint64_t> pre(which.size() + 1, 0);
+            for (size_t i = 0; i < which.size(); i++)
+                pre[i + 1] = pre[i] + std::min(hres[which[i]].nblocks, hjobs[which[i]].blk_cap);
+            HIPCHK(dpre.alloc(pre.size()));
+            HIPCHK(dense.alloc(pre.back() + 1));
+            HIPCHK(hipMemcpyAsync(dpre.p, pre.data(), 8 * pre.size(), hipMemcpyHostToDevice, s));
+            for (size_t i = 0; i < which.size();) {
+                size_t e = i + 1;
+                while (e < which.size() && which[e] == which[e - 1] + 1) e++;
+                HIPCHK(ppg_launch_pack_blocks(s, blk.p, jobs.p + which[i], res.p + which[i], dpre.p + i, dense.p,
+                                              (int)(e - i)));
+                i = e;
+            }
+            std::vector<PpgBlockEnd> hd(pre.back());
+            if (!hd.empty())
+                HIPCHK(hipMemcpyAsync(hd.data(), dense.p, sizeof(PpgBlockEnd) * hd.size(), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (size_t i = 0; i < which.size(); i++)
+                std::copy(hd.begin() + (ptrdiff_t)pre[i], hd.begin() + (ptrdiff_t)pre[i + 1],
+                          hblk.begin() + hjobs[which[i]].blk_off);
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        return PPG_OK;
+    }
+    std::vector<PpgBlockEnd> hblk_big;
+    std::vector<std::vector<PpgBlockEnd>> own_blocks;   // per slot, when decoded into bigblk
+
+    const PpgBlockEnd *blocks(uint32_t q, uint32_t &nb) const {
+        nb = hres[q].nblocks;
+        if (!own_blocks[q].empty()) return own_blocks[q].data();
+        return hblk.data() + hjobs[q].blk_off;
+    }
+};
+
+}  // namespace
+
+static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, const uint8_t *head, int64_t head_n,
+                           const uint8_t trailer[8], uint32_t chunksize, int64_t piece_bytes, int64_t out_capacity,
+                           ppg_index &ix) {
+    const auto t_all = Clock::now();
+    double *stat = ctx->ix_stats;
+    std::fill(stat, stat + 16, 0.0);
+    const int64_t hl = gzip_header_len(head, head_n);
+    if (hl < 0 || len < hl + 8 + 1) return PPG_UNSUPPORTED;
+    Builder B;
+    B.ctx = ctx;
+    B.s = ctx->stream;
+    B.comp = (const uint32_t *)dcomp;
+    B.nwords = (uint64_t)(len + 3) / 4;
+    B.len = len;
+    B.chunksize = chunksize;
+    B.stat = stat;
+    hipStream_t s = B.s;
+    const uint64_t d0 = 8ull * (uint64_t)hl;
+    const uint64_t end_bits = 8ull * (uint64_t)(len - 8);   // no block header starts in the trailer
+    if (piece_bytes <= 0) piece_bytes = std::min<int64_t>(4 << 20, std::max<int64_t>(256 << 10, len / 16384));
+    const uint64_t pbits = 8ull * (uint64_t)piece_bytes;
+
+    // ---- 1. candidate block starts ----
+    auto t = Clock::now();
+    std::vector<uint64_t> lo, hi;
+    for (uint64_t a = d0 + pbits; a < end_bits; a += pbits) {
+        lo.push_back(a);
+        hi.push_back(std::min(a + pbits, end_bits));
+    }
+    std::vector<uint64_t> cand(lo.size());
+    {
+        DevBuf<uint64_t> dlo, dhi, dc;
+        HIPCHK(dlo.alloc(lo.size()));
+        HIPCHK(dhi.alloc(lo.size()));
+        HIPCHK(dc.alloc(lo.size()));
+        if (!lo.empty()) {
+            HIPCHK(hipMemcpyAsync(dlo.p, lo.data(), 8 * lo.size(), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(dhi.p, hi.data(), 8 * lo.size(), hipMemcpyHostToDevice, s));
+            HIPCHK(ppg_launch_block_find(s, B.comp, B.nwords, dlo.p, dhi.p, dc.p, (int)lo.size()));
+            HIPCHK(hipMemcpyAsync(cand.data(), dc.p, 8 * lo.size(), hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    std::vector<Piece> pieces{{0, d0}};
+    for (uint64_t c : cand)
+        if (c != ~0ull) pieces.push_back({(uint32_t)pieces.size(), c});
+    const uint32_t m = (uint32_t)pieces.size();
+    stat[0] = ms_since(t);
+
+    // ---- 2. pass 1: block ends + speculative tails ----
+    t = Clock::now();
+    B.hjobs.resize(m);
+    B.hres.assign(m, PpgInflateResult{});
+    B.own_blocks.assign(m, {});
+    uint64_t nblk_total = 0;
+    for (uint32_t q = 0; q < m; q++) {
+        const uint64_t stop = q + 1 < m ? pieces[q + 1].start : ~0ull;
+        const uint64_t span = (q + 1 < m ? stop : end_bits) - pieces[q].start;
+        PpgInflateJob &J = B.hjobs[q];
+        J = PpgInflateJob{};
+        J.bit_start = pieces[q].start;
+        J.bit_limit = 8ull * (uint64_t)len;
+        J.out_off = (uint64_t)q * kRing;
+        J.dict_off = 0;
+        J.expect_end = ~0ull;
+        J.stop_bit = stop;
+        J.blk_off = (uint32_t)nblk_total;
+        if (span >= (1ull << 31)) return PPG_UNSUPPORTED;   // the decoder's piece-relative bit positions are 32-bit
+        J.blk_cap = (uint32_t)std::min<uint64_t>(span / 8 / 2048 + 64, 1u << 24);
+        nblk_total += J.blk_cap;
+        if (nblk_total >= (1ull << 31)) return PPG_UNSUPPORTED;
+    }
+    B.hblk.assign(nblk_total, PpgBlockEnd{0, 0});
+    HIPCHK(B.jobs.alloc(m));
+    HIPCHK(B.res.alloc(m));
+    HIPCHK(B.blk.alloc(nblk_total));
+    HIPCHK(B.ring.alloc((size_t)m * kRing));
+    HIPCHK(B.tails.alloc((size_t)(m + 1) * kWin));
+    HIPCHK(hipMemsetAsync(B.tails.p, 0, kWin, s));
+    {
+        std::vector<uint32_t> all(m);
+        for (uint32_t q = 0; q < m; q++) all[q] = q;
+        int rc = B.run_pass1(all, false);
+        if (rc) return rc;
+    }
+    stat[1] = ms_since(t);
+
+    // walk the pieces in order: a piece is real iff its predecessor (real) ended at its start
+    t = Clock::now();
+    int redo1 = 0;
+    std::vector<Piece> real;
+    {
+        size_t j = 0;
+        for (;;) {
+            const uint32_t q = pieces[j].slot;
+            PpgInflateResult &r = B.hres[q];
+            if (r.status == PPG_OK && (r.flags & PPG_FLAG_BLK_FULL)) {
+                // more blocks than the slot holds: decode this piece alone into a big list
+                PpgInflateJob &J = B.hjobs[q];
+                const uint64_t span = (J.stop_bit != ~0ull ? J.stop_bit : end_bits) - J.bit_start;
+                J.blk_off = 0;
+                J.blk_cap = (uint32_t)std::min<uint64_t>(span / 10 + 64, 1u << 30);
+                HIPCHK(B.bigblk.alloc(J.blk_cap));
+                int rc = B.run_pass1({q}, true);
+                if (rc) return rc;
+                B.own_blocks[q] = B.hblk_big;
+                redo1++;
+                continue;
+            }
+            if (r.status != PPG_OK || r.nblocks == 0) return r.status != PPG_OK ? r.status : PPG_DATA_ERROR;
+            real.push_back(pieces[j]);
+            if (r.last) break;
+            uint32_t nb = 0;
+            const PpgBlockEnd *bl = B.blocks(q, nb);
+            const uint64_t E = bl[nb - 1].end_bit;
+            // pieces starting inside piece j's last block are false starts: drop them
+            size_t k = j + 1;
+            while (k < pieces.size() && pieces[k].start < E && (k + 1 >= pieces.size() || pieces[k + 1].start <= E)) k++;
+            if (k >= pieces.size()) return PPG_DATA_ERROR;   // a non-final piece must be followed by one
+            if (pieces[k].start != E) {
+                // false start: decode piece k again from the real block end
+                pieces[k].start = E;
+                PpgInflateJob &J = B.hjobs[pieces[k].slot];
+                J.bit_start = E;
+                B.own_blocks[pieces[k].slot].clear();
+                if (J.stop_bit != ~0ull && J.stop_bit <= E) J.stop_bit = E + 1;
+                int rc = B.run_pass1({pieces[k].slot}, false);
+                if (rc) return rc;
+                redo1++;
+            }
+            j = k;
+        }
+    }
+    stat[2] = ms_since(t);
+
+    // ---- 3. pass 2: exact output, batch by batch ----
+    t = Clock::now();
+    const size_t np = real.size();
+    std::vector<uint64_t> U(np), O(np + 1, 0), dict_off(np);
+    size_t max_u = 0;
+    for (size_t j = 0; j < np; j++) {
+        U[j] = B.hres[real[j].slot].produced;
+        O[j + 1] = O[j] + U[j];
+        dict_off[j] = j == 0 ? 0 : (uint64_t)(real[j - 1].slot + 1) * kWin;
+        max_u = std::max<size_t>(max_u, U[j]);
+        if (U[j] >= (1ull << 31)) return PPG_UNSUPPORTED;
+    }
+    const uint64_t total = O[np];
+    uint64_t cap = out_capacity > 0 ? (uint64_t)out_capacity : 0;
+    if (!cap) {
+        size_t fr = 0, tot = 0;
+        HIPCHK(hipMemGetInfo(&fr, &tot));
+        const uint64_t avail = fr > (4ull << 30) ? (uint64_t)fr - (4ull << 30) : (uint64_t)fr / 2;
+        cap = std::min<uint64_t>(total, avail);
+    }
+    cap = std::max<uint64_t>(cap, max_u);
+    DevBuf<uint8_t> out;
+    HIPCHK(out.alloc((size_t)cap + 64));
+    HIPCHK(hipMemsetAsync(out.p + cap, 0, 64, s));
+    DevBuf<PpgInflateJob> jobs2;
+    DevBuf<PpgInflateResult> res2;
+    DevBuf<uint8_t> tmp;                // fresh tails of a batch
+    DevBuf<PpgSpan> spans;
+    DevBuf<PpgAtStats> dstats;
+    DevBuf<uint8_t> dwin;
+    HIPCHK(jobs2.alloc(np));
+    HIPCHK(res2.alloc(np));
+
+    // Core.cs:79-110 state carried across batches
+    const int64_t threshold = (int64_t)(uint32_t)(chunksize - 8u);
+    int64_t records = 0, last_at = -1;
+    int redo2 = 0, rounds2 = 0;
+    uint64_t nblocks_seen = 0;
+    double t_census = 0;
+    ix = ppg_index{};
+    std::vector<uint8_t> zeros(kWin, 0);
+    ix.add_point(0, hl, 0, 0, zeros.data(), nullptr, 0);   // right after the gzip header (Core.cs:101-102)
+
+    std::vector<PpgInflateJob> h2(np);
+    for (size_t j = 0; j < np; j++) {
+        PpgInflateJob &J = h2[j];
+        J = PpgInflateJob{};
+        J.bit_start = real[j].start;
+        J.bit_limit = 8ull * (uint64_t)len;
+        J.out_len = U[j];
+        J.dict_off = dict_off[j];
+        J.expect_end = ~0ull;
+    }
+    size_t b0 = 0;
+    while (b0 < np) {
+        size_t b1 = b0 + 1;
+        while (b1 < np && O[b1 + 1] - O[b0] <= cap) b1++;
+        const size_t nbat = b1 - b0;
+        for (size_t j = b0; j < b1; j++) h2[j].out_off = O[j] - O[b0];
+        HIPCHK(hipMemcpyAsync(jobs2.p + b0, h2.data() + b0, sizeof(PpgInflateJob) * nbat, hipMemcpyHostToDevice, s));
+        std::vector<uint32_t> todo(nbat);
+        for (size_t i = 0; i < nbat; i++) todo[i] = (uint32_t)(b0 + i);
+        HIPCHK(tmp.alloc(nbat * kWin));
+        HIPCHK(B.diff.alloc(nbat));
+        std::vector<PpgInflateResult> r2(nbat);
+        std::vector<uint32_t> hd(nbat);
+        while (!todo.empty()) {
+            rounds2++;
+            // decode (contiguous runs share a launch), then fresh tails vs the ones handed on
+            std::vector<PpgGather> g(todo.size());
+            for (size_t i = 0; i < todo.size();) {
+                size_t e = i + 1;
+                while (e < todo.size() && todo[e] == todo[e - 1] + 1) e++;
+                HIPCHK(ppg_launch_inflate(s, ctx->ring_bits, ctx->lit_bits, B.comp, B.nwords, jobs2.p + todo[i], B.tails.p,
+                                          out.p, res2.p + todo[i], (int)(e - i)));
+                i = e;
+            }
+            for (size_t i = 0; i < todo.size(); i++) {
+                const uint32_t j = todo[i];
+                g[i] = PpgGather{h2[j].out_off, dict_off[j], U[j], ~0ull, (uint64_t)(real[j].slot + 1) * kWin};
+            }
+            HIPCHK(B.gat.alloc(g.size()));
+            HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
+            // fresh tail of todo[i] -> tmp[i], compared with the tail piece todo[i]+1 was given
+            HIPCHK(ppg_launch_gather(s, out.p, B.tails.p, B.gat.p, tmp.p, B.tails.p, B.diff.p, (int)todo.size()));
+            HIPCHK(hipMemcpyAsync(r2.data(), res2.p + b0, sizeof(PpgInflateResult) * nbat, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(hd.data(), B.diff.p, 4 * nbat, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            std::vector<uint32_t> next;
+            for (size_t i = 0; i < todo.size(); i++) {
+                const uint32_t j = todo[i];
+                const PpgInflateResult &r = r2[j - b0];
+                if (r.status != PPG_OK) return r.status;
+                if (r.produced != U[j]) return PPG_DATA_ERROR;
+                if (hd[i]) {
+                    // the history piece j+1 was given is stale: hand on the exact one
+                    HIPCHK(hipMemcpyAsync(B.tail_slot(real[j].slot), tmp.p + i * kWin, kWin, hipMemcpyDeviceToDevice, s));
+                    if (j + 1 < b1) next.push_back(j + 1);
+                }
+            }
+            HIPCHK(hipStreamSynchronize(s));
+            std::sort(next.begin(), next.end());
+            next.erase(std::unique(next.begin(), next.end()), next.end());
+            redo2 += (int)next.size();
+            todo.swap(next);
+        }
+
+        // ---- 4. '@' census of the batch's blocks and the Points among them ----
+        const auto tc = Clock::now();
+        std::vector<PpgSpan> hs;
+        struct BlockRef { uint32_t j; uint64_t end_bit, rel_end; };
+        std::vector<BlockRef> refs;
+        for (size_t j = b0; j < b1; j++) {
+            uint32_t nb = 0;
+            const PpgBlockEnd *bl = B.blocks(real[j].slot, nb);
+            uint64_t prev = 0;
+            for (uint32_t b = 0; b < nb; b++) {
+                hs.push_back(PpgSpan{h2[j].out_off + prev, h2[j].out_off + bl[b].out_end});
+                refs.push_back(BlockRef{(uint32_t)j, bl[b].end_bit, bl[b].out_end});
+                prev = bl[b].out_end;
+            }
+        }
+        std::vector<PpgAtStats> st(hs.size());
+        if (!hs.empty()) {
+            HIPCHK(spans.alloc(hs.size()));
+            HIPCHK(dstats.alloc(hs.size()));
+            HIPCHK(hipMemcpyAsync(spans.p, hs.data(), sizeof(PpgSpan) * hs.size(), hipMemcpyHostToDevice, s));
+            HIPCHK(ppg_launch_at_stats(s, out.p, spans.p, dstats.p, (int)hs.size()));
+            HIPCHK(hipMemcpyAsync(st.data(), dstats.p, sizeof(PpgAtStats) * hs.size(), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        const bool final_batch = b1 == np;
+        struct Pick { int64_t bits, input, output; uint32_t j; uint64_t rel; int64_t off_len; };
+        std::vector<Pick> picks;
+        for (size_t i = 0; i < refs.size(); i++) {
+            const BlockRef &br = refs[i];
+            const uint64_t gs = O[br.j] + (hs[i].lo - h2[br.j].out_off);
+            const uint64_t ge = O[br.j] + br.rel_end;
+            const PpgAtStats &a = st[i];
+            if (a.count) {                                  // SURVEY Q4 (Core.cs:93)
+                const int64_t first = (int64_t)gs + a.first;
+                if (last_at < 0 ? first > kMaxRun : first - last_at > kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
+                if ((int64_t)a.max_gap > kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
+                last_at = (int64_t)gs + a.last;
+                records += a.count;
+            }
+            if (final_batch && i + 1 == refs.size()) break;  // the final block: no Point (data_type & 64)
+            const int64_t input = (int64_t)((br.end_bit + 7) >> 3), bits = input * 8 - (int64_t)br.end_bit;
+            if (ge == 0) {
+                picks.push_back(Pick{bits, input, 0, br.j, 0, -1});
+            } else if (records > threshold) {
+                const int64_t off_len = (int64_t)ge - (last_at < 0 ? 0 : last_at);
+                if (off_len > kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
+                picks.push_back(Pick{bits, input, (int64_t)ge, br.j, br.rel_end, off_len});
+                records = 0;
+            }
+        }
+        nblocks_seen += refs.size();
+        // windows of the picked Points (zero-output Points keep the all-zero window)
+        std::vector<PpgGather> g;
+        for (const Pick &p : picks)
+            if (p.output > 0) g.push_back(PpgGather{h2[p.j].out_off, dict_off[p.j], p.rel, ~0ull, 0});
+        std::vector<uint8_t> hw(g.size() * kWin);
+        if (!g.empty()) {
+            HIPCHK(B.gat.alloc(g.size()));
+            HIPCHK(dwin.alloc(g.size() * kWin));
+            HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
+            HIPCHK(ppg_launch_gather(s, out.p, B.tails.p, B.gat.p, dwin.p, nullptr, nullptr, (int)g.size()));
+            HIPCHK(hipMemcpyAsync(hw.data(), dwin.p, hw.size(), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        size_t wi = 0;
+        for (const Pick &p : picks) {
+            if (p.output == 0) {
+                ix.add_point((int)p.bits, p.input, 0, 0, zeros.data(), nullptr, 0);
+            } else {
+                const uint8_t *w = hw.data() + (wi++) * kWin;
+                ix.add_point((int)p.bits, p.input, p.output, 0, w, w + kWin - p.off_len, (size_t)p.off_len);
+            }
+        }
+        t_census += ms_since(tc);
+        b0 = b1;
+    }
+    stat[3] = ms_since(t) - t_census;
+    stat[4] = t_census;
+
+    // ---- end of the member: trailer (RFC 1952: CRC32, ISIZE) and the final Point (Core.cs:123) ----
+    uint32_t nb = 0;
+    const PpgBlockEnd *bl = B.blocks(real.back().slot, nb);
+    const int64_t tpos = (int64_t)((bl[nb - 1].end_bit + 7) >> 3);
+    if (tpos + 8 > len) return PPG_DATA_ERROR;
+    if (tpos + 8 < len) return PPG_UNSUPPORTED;       // another member or trailing bytes
+    const uint32_t isize = (uint32_t)trailer[4] | ((uint32_t)trailer[5] << 8) | ((uint32_t)trailer[6] << 16) |
+                           ((uint32_t)trailer[7] << 24);
+    if (isize != (uint32_t)total) return PPG_DATA_ERROR;
+    if (last_at < 0 ? (int64_t)total > kMaxRun : (int64_t)total - 1 - last_at >= kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
+    {
+        std::vector<uint8_t> w(kWin);
+        HIPCHK(hipMemcpy(w.data(), B.tail_slot(real.back().slot), kWin, hipMemcpyDeviceToHost));
+        ix.add_point(0, len, (int64_t)total, 0, w.data(), nullptr, 0);
+    }
+    stat[5] = ms_since(t_all);
+    stat[6] = (double)m;
+    stat[7] = (double)np;
+    stat[8] = (double)redo1;
+    stat[9] = (double)redo2;
+    stat[10] = (double)rounds2;
+    stat[11] = (double)nblocks_seen;
+    stat[12] = (double)ix.pts.size();
+    stat[13] = (double)total;
+    return PPG_OK;
+}
+
+extern "C" {
+
+int ppg_index_build_gpu(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
+                        int64_t piece_bytes, int64_t out_capacity, ppg_index **out) {
+    if (!ctx || !gz || gz_len <= 0 || !out) return PPG_ARG_ERROR;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t hn = std::min<int64_t>(gz_len, 65536);
+    std::vector<uint8_t> head((size_t)hn);
+    uint8_t trailer[8] = {0};
+    DevBuf<uint8_t> own;
+    const uint8_t *d = (const uint8_t *)gz;
+    if (gz_on_device) {
+        if (((uintptr_t)gz & 3) != 0) return PPG_ARG_ERROR;
+        HIPCHK(hipMemcpy(head.data(), gz, (size_t)hn, hipMemcpyDeviceToHost));
+        if (gz_len >= 8) HIPCHK(hipMemcpy(trailer, d + gz_len - 8, 8, hipMemcpyDeviceToHost));
+    } else {
+        memcpy(head.data(), gz, (size_t)hn);
+        if (gz_len >= 8) memcpy(trailer, d + gz_len - 8, 8);
+        HIPCHK(own.alloc((size_t)gz_len + 64));
+        HIPCHK(hipMemsetAsync(own.p + gz_len, 0, 64, s));
+        HIPCHK(hipMemcpyAsync(own.p, gz, (size_t)gz_len, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        d = own.p;
+    }
+    auto ix = std::make_unique<ppg_index>();
+    const int rc = build_index_gpu(ctx, d, gz_len, head.data(), hn, trailer, chunksize, piece_bytes, out_capacity, *ix);
+    if (rc != PPG_OK) return rc;
+    *out = ix.release();
+    return PPG_OK;
+}
+
+int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksize, int64_t piece_bytes,
+                             ppg_index **out) {
+    if (!ctx || !gz_path || !out) return PPG_ARG_ERROR;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int fd = open(gz_path, O_RDONLY);
+    if (fd < 0) return PPG_IO_ERROR;
+    struct FdClose { int fd; ~FdClose() { close(fd); } } fdc{fd};
+    const int64_t len = (int64_t)lseek(fd, 0, SEEK_END);
+    if (len <= 0) return PPG_DATA_ERROR;
+    // whole member into HBM: pread into two pinned 64 MiB halves, H2D alternating
+    const auto t0 = std::chrono::steady_clock::now();
+    DevBuf<uint8_t> dev;
+    HIPCHK(dev.alloc((size_t)len + 64));
+    HIPCHK(hipMemsetAsync(dev.p + len, 0, 64, s));
+    constexpr int64_t kStage = 64 << 20;
+    PinnedBuf pin;
+    HIPCHK(pin.alloc(2 * kStage));
+    hipEvent_t ev[2];
+    HIPCHK(hipEventCreate(&ev[0]));
+    HIPCHK(hipEventCreate(&ev[1]));
+    struct EvFree { hipEvent_t *e; ~EvFree() { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); } } evf{ev};
+    bool used[2] = {false, false};
+    int64_t done = 0;
+    for (int h = 0; done < len; h ^= 1) {
+        if (used[h]) HIPCHK(hipEventSynchronize(ev[h]));
+        const int64_t n = std::min(kStage, len - done);
+        uint8_t *p = pin.p + h * kStage;
+        int64_t got = 0;
+        while (got < n) {
+            const ssize_t r = pread(fd, p + got, (size_t)(n - got), (off_t)(done + got));
+            if (r <= 0) return PPG_IO_ERROR;
+            got += r;
+        }
+        HIPCHK(hipMemcpyAsync(dev.p + done, p, (size_t)n, hipMemcpyHostToDevice, s));
+        HIPCHK(hipEventRecord(ev[h], s));
+        used[h] = true;
+        done += n;
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t hn = std::min<int64_t>(len, 65536);
+    std::vector<uint8_t> head((size_t)hn);
+    uint8_t trailer[8] = {0};
+    if (pread(fd, head.data(), (size_t)hn, 0) != (ssize_t)hn) return PPG_IO_ERROR;
+    if (len >= 8 && pread(fd, trailer, 8, (off_t)(len - 8)) != 8) return PPG_IO_ERROR;
+    auto ix = std::make_unique<ppg_index>();
+    const double upload = ms_since(t0);
+    const int rc = build_index_gpu(ctx, dev.p, len, head.data(), hn, trailer, chunksize, piece_bytes, 0, *ix);
+    ctx->ix_stats[14] = upload;
+    if (rc != PPG_OK) return rc;
+    *out = ix.release();
+    return PPG_OK;
+}
+
+int ppg_index_build_gpu_stats(ppg_ctx *ctx, double *vals, int32_t n) {
+    if (!ctx || !vals || n < 0) return PPG_ARG_ERROR;
+    for (int32_t i = 0; i < n && i < 16; i++) vals[i] = ctx->ix_stats[i];
+    return PPG_OK;
+}
+
+}  // extern "C"

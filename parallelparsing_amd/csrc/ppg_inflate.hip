@@ -28,6 +28,11 @@
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 
+// CreateIndex pass 1 (IX): each job's output lives in a 64 KiB ring of the out buffer (only the
+// last 32 KiB + REACH are ever read back)
+#define IX_RING_BYTES 65536u
+#define IX_RING_MASK (IX_RING_BYTES - 1u)
+
 template <int RB, int LBT>
 struct __attribute__((aligned(16))) InflateLds {
     uint8_t ring[1u << RB];
@@ -156,17 +161,19 @@ __device__ __forceinline__ void flush_range(const uint8_t *ring, uint8_t *out, u
 // earlier stores — a wave's accesses to one address are ordered) or the Point's window.  Read as
 // an aligned dword from a uniform base + 32-bit lane offset (global_load saddr form; never merged
 // with an LDS byte load into a flat load).  ob: out + (out_off & ~3), oa: out_off & 3.
+// IX (CreateIndex pass 1): the job's output is a 64 KiB ring, position p at ob[p & 0xFFFF].
+template <bool IX = false>
 __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, const uint8_t *dict, int32_t p) {
     // the two loads differ in width so the compiler cannot fold them into one per-lane base select
     if (p >= 0) {
-        const uint32_t q = oa + (uint32_t)p;
+        const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
         return (*(const uint32_t *)(ob + (q & ~3u)) >> (8 * (q & 3))) & 255u;
     }
     return dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
 }
 
 // One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
-template <int RB>
+template <int RB, bool IX>
 __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uint32_t oa, const uint8_t *dict,
                                            uint32_t rb0, uint32_t pos, uint32_t dist, uint32_t n, int lane) {
     constexpr uint32_t RM = (1u << RB) - 1;
@@ -197,7 +204,7 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uin
                 const int32_t rel = (int32_t)pos - (int32_t)back;
                 uint32_t v;
                 if (back + n <= REACH) v = ring[(dst0 - back) & RM];
-                else v = far_byte(ob, oa, dict, rel);
+                else v = far_byte<IX>(ob, oa, dict, rel);
                 ring[(dst0 + j) & RM] = (uint8_t)v;
             }
         }
@@ -233,11 +240,15 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     return (tok & ~sm) | (spec & sm);
 }
 
-template <int RB, int LBT>
+// IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
+// IX = true:  CreateIndex pass 1 (ppg_index_gpu.cpp): decode whole blocks from a candidate block
+//             start until a block ends at or past stop_bit, recording every block end.
+template <int RB, int LBT, bool IX>
 __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
-                                                         PpgInflateResult *__restrict__ res, int njobs) {
+                                                         PpgInflateResult *__restrict__ res, int njobs,
+                                                         PpgBlockEnd *__restrict__ blk) {
     constexpr uint32_t RING = 1u << RB;
     constexpr uint32_t RM = RING - 1;
     // flush unit: far references (older than REACH = RING - 64) must already be flushed; a round
@@ -251,7 +262,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     if (k >= njobs) return;
     const PpgInflateJob J = jobs[k];
     const uint64_t out_off = J.out_off;
-    const uint32_t len = (uint32_t)J.out_len;       // host guarantees < 2^31
+    const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // host guarantees < 2^31
     const uint32_t rb0 = (uint32_t)out_off;         // ring slot of chunk position p: (rb0 + p) & RM
     const uint8_t *dict = dicts + J.dict_off;       // chunk position p < 0 is dict[32768 + p]
     const uint8_t *ob = out + (out_off & ~3ull);    // chunk position p >= 0 is ob[oa + p]
@@ -284,6 +295,24 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
     uint32_t fl_next = UNIT - (uint32_t)(out_off & (UNIT - 1));   // next global 4 KiB boundary
     int status = ST_OK, flags = 0, last = 0, in_block = 0;
     Canon clit = {0, 0, 0}, cdst = {0, 0, 0};   // per-lane canonical codes of the current block
+    // flush of chunk positions [lo, hi) (never across a UNIT boundary except the plain case)
+    auto flush = [&](uint32_t lo, uint32_t hi) {
+        if constexpr (IX) {
+            const uint64_t g = out_off + (lo & IX_RING_MASK);
+            flush_range<RB>(S.ring, out, g, g + (hi - lo), lane);
+        } else {
+            flush_range<RB>(S.ring, out, out_off + lo, out_off + hi, lane);
+        }
+    };
+    uint32_t nblk = 0;
+    // IX: record a block end (chunk-relative bit e); false = stop decoding
+    auto block_end = [&](uint32_t e) -> bool {
+        if (nblk >= J.blk_cap) { flags |= PPG_FLAG_BLK_FULL; return false; }
+        if (lane == 0) blk[J.blk_off + nblk] = PpgBlockEnd{w0abs * 32 + e, pos};
+        nblk++;
+        return w0abs * 32 + e < J.stop_bit;
+    };
+
 
     while (pos < len && !last) {
         r.sg = uni(r.sg);
@@ -317,7 +346,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 pos += piece;
                 copied += piece;
                 if (pos >= fl_next) {
-                    flush_range<RB>(S.ring, out, out_off + fl_done, out_off + fl_next, lane);
+                    flush(fl_done, fl_next);
                     fl_done = fl_next;
                     fl_next += UNIT;
                 }
@@ -325,6 +354,9 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             rd_seek(r, S.stream, (bytepos + copied) * 8, lane);
             if (copied < slen) break;   // output full mid-block (zlib stops at avail_out == 0)
             in_block = 0;
+            if constexpr (IX) {
+                if (!block_end((bytepos + copied) * 8)) break;
+            }
             continue;
         }
         if (type == 3) { status = ST_DATA_ERROR; break; }
@@ -476,7 +508,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 if (jj < -(int32_t)(RING - 64))                       // far (literals: jj >= -512)
-                    val = far_byte(ob, oa, dict, (int32_t)pos + jj);
+                    val = far_byte<IX>(ob, oa, dict, (int32_t)pos + jj);
                 const bool dep = jj >= 0;                             // produced in this round
                 if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
@@ -496,11 +528,14 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
             }
             pos += rout;
             if (pos >= fl_next) {
-                flush_range<RB>(S.ring, out, out_off + fl_done, out_off + fl_next, lane);
+                flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
             bp += s;
+            if constexpr (IX) {   // past the member, or runaway output (a false start)
+                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
+            }
             if (!spec) continue;
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
@@ -522,20 +557,24 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
                 if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
                 const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
                 const uint32_t n = min(ml, len - pos);
-                copy_match<RB>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
+                copy_match<RB, IX>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
             }
             bp = rd_pos(r);
             if (pos >= fl_next) {
-                flush_range<RB>(S.ring, out, out_off + fl_done, out_off + fl_next, lane);
+                flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
         }
         if (status != ST_OK) break;
         rd_seek(r, S.stream, bp, lane);   // the next block header / the R-E5 check read from bp
+        if constexpr (IX) {
+            if (in_block) { status = ST_DATA_ERROR; break; }   // output limit inside a block
+            if (!block_end(bp)) break;
+        }
     }
-    flush_range<RB>(S.ring, out, out_off + fl_done, out_off + pos, lane);
+    flush(fl_done, pos);
 
     // zlib was handed only the chunk's slice (LazyFileReader.cs:63-69): needing bits past it is
     // the DATA_ERROR of Core.cs:174.  R-E5: the next symbol should be the block's end-of-block.
@@ -544,7 +583,7 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         flags |= PPG_FLAG_OVERRUN;
         if (status == ST_OK) status = ST_DATA_ERROR;
     }
-    if (status == ST_OK && in_block && pos == len) {
+    if (!IX && status == ST_OK && in_block && pos == len) {
         rd_refill(r, S.stream, lane);
         if (canon_decode(r, clit, S.lit_sorted, lane) == 256) end_bit = rd_pos(r);
         else flags |= PPG_FLAG_NO_EOB;
@@ -554,6 +593,8 @@ __global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restr
         res[k].end_bit = w0abs * 32 + end_bit;
         res[k].status = status;
         res[k].flags = flags;
+        res[k].nblocks = nblk;
+        res[k].last = (uint32_t)last;
     }
 }
 
@@ -576,11 +617,21 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
     if (njobs <= 0) return hipSuccess;
 #define X(R, L)                                                                                               \
     if (ring_bits == R && lit_bits == L) {                                                                    \
-        hipLaunchKernelGGL((ppg_inflate_kernel<R, L>), dim3(njobs), dim3(64), sizeof(InflateLds<R, L>), s, comp, \
-                           nwords, jobs, dicts, out, res, njobs);                                             \
+        hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false>), dim3(njobs), dim3(64), sizeof(InflateLds<R, L>), s, \
+                           comp, nwords, jobs, dicts, out, res, njobs, nullptr);                             \
         return hipGetLastError();                                                                             \
     }
     PPG_VARIANTS(X)
 #undef X
     return hipErrorInvalidValue;
+}
+
+// CreateIndex pass 1: jobs decode whole blocks into 64 KiB output rings (out + k * 64 KiB)
+hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
+                                 const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
+                                 int njobs) {
+    if (njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true>), dim3(njobs), dim3(64), sizeof(InflateLds<10, 8>), s, comp,
+                       nwords, jobs, dicts, out, res, njobs, blk);
+    return hipGetLastError();
 }
