@@ -105,6 +105,65 @@ def ingest_run(tf, ix, dev):
             os.remove(path)
 
 
+def create_index_run(tf, args, dev):
+    """GPU CreateIndex (ppg_index_build_gpu) over the whole member resident in HBM, checked Point by
+    Point against the member's exactly derived index, beside the host zlib CreateIndex (the
+    reference's algorithm, IndexBuilder) timed on one segment of the same data."""
+    import torch
+    import parallelparsing_amd as pp
+    from parallelparsing_amd.tiled import TiledFile
+    gz = torch.empty(tf.file_len + 256, dtype=torch.uint8, device=dev)
+    gz[tf.file_len:].zero_()
+    tf.fill_device(gz, 0, tf.file_len)
+    torch.cuda.synchronize()
+    g = gz[: tf.file_len]
+    runs = []
+    ix = None
+    for _ in range(2):                                             # first run: allocation warm-up
+        ix = None
+        t = time.perf_counter()
+        ix = pp.Core.BuildDeflateIndexGpu(g, args.chunk)
+        runs.append(time.perf_counter() - t)
+        log(f"[bench] GPU CreateIndex: {runs[-1]:.2f} s, {ix.Count} points")
+    st = pp.Core.gpu_index_stats()
+    del gz, g
+    torch.cuda.empty_cache()
+    out, inp, bits = ix.arrays()
+    ok = (ix.Count == tf.npoints and (out == tf.p_output).all() and (inp == tf.p_input).all()
+          and (bits == tf.p_bits).all())
+    if ok:
+        win, offs = tf.windows(0, tf.npoints)
+        ok = bool(np.array_equal(ix.windows_array(), win))
+        o = 0
+        for i in range(tf.npoints):
+            n = int(tf.p_offlen[i])
+            ok = ok and ix[i].offset == offs[o:o + n].tobytes() if n else ok and ix.point_fields(i)[3] == 0
+            o += n
+    assert ok, "GPU CreateIndex differs from the member's index"
+    log("[bench] GPU CreateIndex verified against the member's index")
+    sec = runs[-1]
+    text = tf.text_len * tf.repeats
+    # host CreateIndex (serial zlib Z_BLOCK pass) on a one-segment member of the same data
+    one = TiledFile(args.seg_records, 1, args.chunk, threads=args.host_threads)
+    one_gz = one.file_bytes(0, one.file_len)
+    t = time.perf_counter()
+    cix = pp.Core.BuildDeflateIndex(one_gz, args.chunk)
+    csec = time.perf_counter() - t
+    assert cix.Count == one.npoints
+    cpu_gbs = one.text_len / csec / 1e9
+    return {"seconds": sec, "first_run_s": runs[0], "points": ix.Count, "gz_GBps": tf.file_len / sec / 1e9,
+            "decompressed_GBps": text / sec / 1e9,
+            "phases_ms": {k: round(st[k], 2) for k in ("finder_ms", "pass1_ms", "chain_ms", "resolve_ms", "pass2_ms",
+                                                       "census_ms")},
+            "pieces": int(st["pieces"]), "real_pieces": int(st["real_pieces"]), "redo1": int(st["redo1"]),
+            "pass2_batches": int(st["batches"]),
+            "blocks": int(st["blocks"]), "verified": "every Point (Output, Input, Bits, Window, offset) of the member",
+            "cpu_reference": {"seconds": csec, "decompressed_GBps": cpu_gbs, "cores": 1,
+                              "sample": f"host zlib CreateIndex (Core.cs:14-131 restated) of a 1-segment member "
+                                        f"({one.file_len / 1e9:.2f} GB gz, {one.npoints} points)",
+                              "projected_seconds_full_member": text / 1e9 / cpu_gbs}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,6 +176,8 @@ def main():
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--create-index", action="store_true",
+                    help="also time the GPU CreateIndex over the whole member (reported under 'create_index')")
     ap.add_argument("--ingest", action="store_true",
                     help="also time DecompressAll straight from the .gz file on disk (host ingest, PCIe-inclusive; "
                          "reported under 'ingest', never as value)")
@@ -234,9 +295,12 @@ def main():
                      "mean_launch_ms": mean_launch_s * 1e3},
         "reference_published_rec_s": REFERENCE_REC_S,
     }
-    if rank == 0 and world == 1 and args.ingest:
+    if rank == 0 and world == 1 and (args.ingest or args.create_index):
         del shard, comp
         torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and args.create_index:
+        line["create_index"] = create_index_run(tf, args, dev)
+    if rank == 0 and world == 1 and args.ingest:
         line["ingest"] = ingest_run(tf, tf.index(0, tf.npoints), ctx)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)

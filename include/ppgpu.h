@@ -66,7 +66,7 @@ int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksi
                              ppg_index **out);
 /* Last GPU CreateIndex on ctx: [0] finder ms, [1] pass-1 ms, [2] chain check ms, [3] pass-2 ms,
  * [4] census + windows ms, [5] total ms, [6] pieces, [7] real pieces, [8] pass-1 redos,
- * [9] pass-2 redos, [10] pass-2 rounds, [11] blocks, [12] points, [13] output bytes,
+ * [9] history resolve ms, [10] pass-2 batches, [11] blocks, [12] points, [13] output bytes,
  * [14] file upload ms (ppg_index_build_gpu_file). */
 int ppg_index_build_gpu_stats(ppg_ctx *ctx, double *vals, int32_t n);
 

@@ -90,6 +90,13 @@ class Index:
             out[i], inp[i], bits[i], _ = self.point_fields(i)
         return out, inp, bits
 
+    def windows_array(self):
+        """All Point windows as one uint8 array (Count * 32768; the index stores them contiguously)."""
+        n = self.Count
+        if n == 0:
+            return np.zeros(0, np.uint8)
+        return np.frombuffer(C.string_at(lib.ppg_index_window(self._h, 0), n * WINSIZE), np.uint8)
+
     @staticmethod
     def from_points(output, inp, bits, windows, offset_len, offsets, chunk_max_bytes=0):
         """Index from arrays (ppg_index_from_points): windows is count*32768 bytes."""
@@ -258,7 +265,8 @@ class Core:
         return Index(h.value)
 
     GPU_INDEX_STATS = ("finder_ms", "pass1_ms", "chain_ms", "pass2_ms", "census_ms", "total_ms", "pieces",
-                       "real_pieces", "redo1", "redo2", "rounds2", "blocks", "points", "output_bytes", "upload_ms")
+                       "real_pieces", "redo1", "resolve_ms", "batches", "blocks", "points", "output_bytes",
+                       "upload_ms")
 
     @staticmethod
     def gpu_index_stats(device=None):

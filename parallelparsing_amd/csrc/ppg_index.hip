@@ -9,6 +9,7 @@
 //   ppg_gather_kernel       32 KiB histories ending at a given output position (piece tails,
 //                           Point windows), optionally compared against a previous copy
 //   ppg_at_stats_kernel     per-block '@' count / first / last / largest gap (Core.cs:79-96)
+//   ppg_resolve_kernel      exact starting histories of all pieces from their symbolic tails
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "ppg_device.h"
@@ -246,6 +247,45 @@ hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const P
                                   const PpgInflateResult *res, const uint64_t *pre, PpgBlockEnd *dense, int n) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(ppg_pack_blocks_kernel, dim3(n), dim3(256), 0, s, blk, jobs, res, pre, dense, n);
+    return hipGetLastError();
+}
+
+// Symbolic tails: pass 1 decodes every piece twice, with history patterns A[i] = i & 0xFF and
+// B[i] = ((i >> 8) + 1 + (i & 0xFF)) & 0xFF.  Decoding only copies bytes, so an output byte is
+// either a literal (x == y in both runs) or history byte i (x = A[i], y = B[i], x != y, and
+// i = ((((y - x) & 0xFF) - 1) << 8) | x).  Piece j+1 starts with piece j's last 32 KiB, so
+//   W[j+1][t] = x == y ? x : W[j][i(x, y)],   W[0] = zeros (the stream start),
+// one 32 KiB gather per piece, in piece order (a single workgroup walks the chain).
+__global__ __launch_bounds__(1024) void ppg_resolve_kernel(const uint8_t *__restrict__ ta,
+                                                           const uint8_t *__restrict__ tb,
+                                                           const uint32_t *__restrict__ slots, int np,
+                                                           uint8_t *W) {
+    for (int j = 0; j < np; j++) {
+        const uint8_t *src = W + (uint64_t)j * 32768;
+        uint8_t *dst = W + (uint64_t)(j + 1) * 32768;
+        const uint32_t *a = (const uint32_t *)(ta + (uint64_t)slots[j] * 32768);
+        const uint32_t *b = (const uint32_t *)(tb + (uint64_t)slots[j] * 32768);
+        uint32_t *d = (uint32_t *)dst;
+        for (uint32_t t = threadIdx.x; t < 8192; t += 1024) {
+            const uint32_t xa = a[t], xb = b[t];
+            uint32_t v = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t x = (xa >> (8 * q)) & 255u, y = (xb >> (8 * q)) & 255u;
+                const uint32_t byte = x == y ? x : src[((((y - x) & 255u) - 1u) << 8) | x];
+                v |= byte << (8 * q);
+            }
+            d[t] = v;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
+hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
+                              uint8_t *W) {
+    if (np <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_resolve_kernel, dim3(1), dim3(1024), 0, s, ta, tb, slots, np, W);
     return hipGetLastError();
 }
 

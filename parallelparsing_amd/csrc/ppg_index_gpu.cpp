@@ -9,19 +9,21 @@
 //   1. finder     the compressed member is cut into pieces of piece_bytes; one wave per piece
 //                 finds the first bit where a dynamic-block header zlib would accept starts
 //                 (ppg_block_find_kernel).  Piece 0 starts right after the gzip header.
-//   2. pass 1     every piece decodes whole blocks from its candidate with an all-zero history
-//                 until a block ends at or past the next piece's candidate, recording each block
-//                 end (ppg_inflate_kernel IX).  Block boundaries do not depend on history bytes,
-//                 so walking the pieces in order proves each start: piece j+1 is real iff the
-//                 (real) piece j ended exactly there; otherwise piece j+1 is redone from where
-//                 piece j really ended.  Each piece leaves its last 32 KiB (its "tail").
-//   3. pass 2     every piece is decoded again (the DecompressAll kernel) with the previous
-//                 piece's pass-1 tail as history.  Piece 0's history is exact (none), so by
-//                 induction piece j is exact iff the tail it was given equals the tail piece j-1
-//                 now produces; pieces whose history changed are redone until nothing changes.
-//                 In practice pass-1 tails are already exact (a piece's last 32 KiB essentially
-//                 never copies from its own starting history), so pass 2 runs once.
-//   4. census     per-block '@' statistics over the exact output (ppg_at_stats_kernel); the host
+//   2. pass 1     every piece decodes whole blocks from its candidate until a block ends at or
+//                 past the next piece's candidate, recording each block end (ppg_inflate_kernel
+//                 IX).  Block boundaries do not depend on history bytes, so walking the pieces in
+//                 order proves each start: piece j+1 is real iff the (real) piece j ended exactly
+//                 there; otherwise piece j+1 is redone from where piece j really ended.  The
+//                 history is unknown, so each piece decodes twice with two synthetic histories;
+//                 the two versions of its last 32 KiB (its "tail") tell every byte apart as a
+//                 literal or a copy of history byte i (ppg_resolve_kernel).  FASTQ needs this:
+//                 a header's "length=150" is copied from the previous record's, a chain that runs
+//                 back to the piece's start, so tails depend on the starting history.
+//   3. resolve    the exact starting history of every piece, walking the chain of symbolic
+//                 tails from the stream start (one 32 KiB gather per piece).
+//   4. pass 2     every piece decoded again with its exact history (the DecompressAll kernel);
+//                 its tail must reproduce the resolved history of the next piece.
+//   5. census     per-block '@' statistics over the exact output (ppg_at_stats_kernel); the host
 //                 walks the blocks in order exactly as Core.cs:98-110 does and gathers the 32 KiB
 //                 windows of the chosen Points on the GPU (ppg_gather_kernel).
 //
@@ -45,6 +47,8 @@ hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t n
 hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
                              const uint8_t *ref, uint32_t *diff, int n);
 hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan *spans, PpgAtStats *st, int n);
+hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
+                              uint8_t *W);
 hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const PpgInflateJob *jobs,
                                   const PpgInflateResult *res, const uint64_t *pre, PpgBlockEnd *dense, int n);
 
@@ -98,42 +102,57 @@ struct Builder {
     DevBuf<PpgInflateResult> res;
     DevBuf<PpgBlockEnd> blk, bigblk;
     DevBuf<uint8_t> ring;
-    DevBuf<uint8_t> tails;              // slot 0: zeros; slot q + 1: tail of pass-1 job q
+    DevBuf<uint8_t> pat;                // synthetic histories A (offset 0) and B (offset 32 KiB)
+    DevBuf<uint8_t> ta, tb;             // tails of pass-1 job q at q * 32 KiB, runs A and B
+    std::vector<PpgInflateResult> hres_b;
     DevBuf<PpgGather> gat;
     DevBuf<uint32_t> diff;
     DevBuf<uint64_t> dpre;
     DevBuf<PpgBlockEnd> dense;
 
-    uint8_t *tail_slot(uint32_t q) { return tails.p + (uint64_t)(q + 1) * kWin; }
-
-    // pass-1 decode of job slots `which` (ascending); refreshes their results, blocks and tails
+    // pass-1 decode of job slots `which` (ascending), once per synthetic history; refreshes
+    // their results, block lists and both tails
     int run_pass1(const std::vector<uint32_t> &which, bool big) {
         if (which.empty()) return PPG_OK;
-        // contiguous runs launch as one grid; the common case is all slots at once
-        for (size_t i = 0; i < which.size();) {
-            size_t e = i + 1;
-            while (e < which.size() && which[e] == which[e - 1] + 1 && !big) e++;
-            const uint32_t q0 = which[i], n = (uint32_t)(e - i);
-            HIPCHK(hipMemcpyAsync(jobs.p + q0, hjobs.data() + q0, sizeof(PpgInflateJob) * n, hipMemcpyHostToDevice, s));
-            HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jobs.p + q0, tails.p, ring.p, res.p + q0,
-                                         big ? bigblk.p : blk.p, (int)n));
-            HIPCHK(hipMemcpyAsync(hres.data() + q0, res.p + q0, sizeof(PpgInflateResult) * n, hipMemcpyDeviceToHost, s));
-            i = e;
+        for (int run = 0; run < 2; run++) {
+            std::vector<PpgInflateResult> &hr = run ? hres_b : hres;
+            for (uint32_t q : which) hjobs[q].dict_off = run ? (uint64_t)kWin : 0;
+            // contiguous runs launch as one grid; the common case is all slots at once
+            for (size_t i = 0; i < which.size();) {
+                size_t e = i + 1;
+                while (e < which.size() && which[e] == which[e - 1] + 1 && !big) e++;
+                const uint32_t q0 = which[i], n = (uint32_t)(e - i);
+                HIPCHK(hipMemcpyAsync(jobs.p + q0, hjobs.data() + q0, sizeof(PpgInflateJob) * n, hipMemcpyHostToDevice,
+                                      s));
+                HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jobs.p + q0, pat.p, ring.p, res.p + q0,
+                                             big ? bigblk.p : blk.p, (int)n));
+                HIPCHK(hipMemcpyAsync(hr.data() + q0, res.p + q0, sizeof(PpgInflateResult) * n, hipMemcpyDeviceToHost,
+                                      s));
+                i = e;
+            }
+            HIPCHK(hipStreamSynchronize(s));
+            // this run's tails (before the next run reuses the rings)
+            std::vector<PpgGather> g(which.size());
+            for (size_t i = 0; i < which.size(); i++) {
+                const uint32_t q = which[i];
+                g[i] = PpgGather{(uint64_t)q * kRing, run ? (uint64_t)kWin : 0, hr[q].produced, kRing - 1, 0};
+            }
+            HIPCHK(gat.alloc(g.size()));
+            HIPCHK(hipMemcpyAsync(gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
+            uint8_t *tails = run ? tb.p : ta.p;
+            for (size_t i = 0; i < which.size();) {   // one gather per contiguous run of slots
+                size_t e = i + 1;
+                while (e < which.size() && which[e] == which[e - 1] + 1) e++;
+                HIPCHK(ppg_launch_gather(s, ring.p, pat.p, gat.p + i, tails + (uint64_t)which[i] * kWin, nullptr,
+                                         nullptr, (int)(e - i)));
+                i = e;
+            }
+            HIPCHK(hipStreamSynchronize(s));
         }
-        HIPCHK(hipStreamSynchronize(s));
-        // tails and block lists
-        std::vector<PpgGather> g(which.size());
-        for (size_t i = 0; i < which.size(); i++) {
-            const uint32_t q = which[i];
-            g[i] = PpgGather{(uint64_t)q * kRing, 0, hres[q].produced, kRing - 1, 0};
-        }
-        HIPCHK(gat.alloc(g.size()));
-        HIPCHK(hipMemcpyAsync(gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
-        for (size_t i = 0; i < which.size();) {     // one gather per contiguous run (dst = tail slots)
-            size_t e = i + 1;
-            while (e < which.size() && which[e] == which[e - 1] + 1) e++;
-            HIPCHK(ppg_launch_gather(s, ring.p, tails.p, gat.p + i, tail_slot(which[i]), nullptr, nullptr, (int)(e - i)));
-            i = e;
+        for (uint32_t q : which) {   // both runs follow the same bits: same blocks, same sizes
+            const PpgInflateResult &a = hres[q], &b = hres_b[q];
+            if (a.status != b.status || a.produced != b.produced || a.nblocks != b.nblocks || a.end_bit != b.end_bit)
+                return PPG_DEVICE_ERROR;
         }
         if (big) {
             const uint32_t q = which[0];
@@ -231,6 +250,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     t = Clock::now();
     B.hjobs.resize(m);
     B.hres.assign(m, PpgInflateResult{});
+    B.hres_b.assign(m, PpgInflateResult{});
     B.own_blocks.assign(m, {});
     uint64_t nblk_total = 0;
     for (uint32_t q = 0; q < m; q++) {
@@ -255,8 +275,17 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     HIPCHK(B.res.alloc(m));
     HIPCHK(B.blk.alloc(nblk_total));
     HIPCHK(B.ring.alloc((size_t)m * kRing));
-    HIPCHK(B.tails.alloc((size_t)(m + 1) * kWin));
-    HIPCHK(hipMemsetAsync(B.tails.p, 0, kWin, s));
+    HIPCHK(B.ta.alloc((size_t)m * kWin));
+    HIPCHK(B.tb.alloc((size_t)m * kWin));
+    {
+        std::vector<uint8_t> pat(2 * kWin);
+        for (int i = 0; i < kWin; i++) {
+            pat[i] = (uint8_t)(i & 255);
+            pat[kWin + i] = (uint8_t)(((i >> 8) + 1 + (i & 255)) & 255);
+        }
+        HIPCHK(B.pat.alloc(pat.size()));
+        HIPCHK(hipMemcpy(B.pat.p, pat.data(), pat.size(), hipMemcpyHostToDevice));
+    }
     {
         std::vector<uint32_t> all(m);
         for (uint32_t q = 0; q < m; q++) all[q] = q;
@@ -313,15 +342,30 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     }
     stat[2] = ms_since(t);
 
-    // ---- 3. pass 2: exact output, batch by batch ----
+    // ---- 3. exact starting histories from the symbolic tails ----
     t = Clock::now();
     const size_t np = real.size();
-    std::vector<uint64_t> U(np), O(np + 1, 0), dict_off(np);
+    DevBuf<uint8_t> W;                  // W[j]: history of real piece j; W[np]: the member's last 32 KiB
+    HIPCHK(W.alloc((np + 1) * kWin));
+    HIPCHK(hipMemsetAsync(W.p, 0, kWin, s));
+    {
+        std::vector<uint32_t> sl(np);
+        for (size_t j = 0; j < np; j++) sl[j] = real[j].slot;
+        DevBuf<uint32_t> dsl;
+        HIPCHK(dsl.alloc(np));
+        HIPCHK(hipMemcpyAsync(dsl.p, sl.data(), 4 * np, hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_resolve(s, B.ta.p, B.tb.p, dsl.p, (int)np, W.p));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    stat[9] = ms_since(t);
+
+    // ---- 4. pass 2: exact output, batch by batch ----
+    t = Clock::now();
+    std::vector<uint64_t> U(np), O(np + 1, 0);
     size_t max_u = 0;
     for (size_t j = 0; j < np; j++) {
         U[j] = B.hres[real[j].slot].produced;
         O[j + 1] = O[j] + U[j];
-        dict_off[j] = j == 0 ? 0 : (uint64_t)(real[j - 1].slot + 1) * kWin;
         max_u = std::max<size_t>(max_u, U[j]);
         if (U[j] >= (1ull << 31)) return PPG_UNSUPPORTED;
     }
@@ -339,7 +383,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     HIPCHK(hipMemsetAsync(out.p + cap, 0, 64, s));
     DevBuf<PpgInflateJob> jobs2;
     DevBuf<PpgInflateResult> res2;
-    DevBuf<uint8_t> tmp;                // fresh tails of a batch
+    DevBuf<uint8_t> tmp;                // pass-2 tails of a batch (checked against W)
     DevBuf<PpgSpan> spans;
     DevBuf<PpgAtStats> dstats;
     DevBuf<uint8_t> dwin;
@@ -349,7 +393,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     // Core.cs:79-110 state carried across batches
     const int64_t threshold = (int64_t)(uint32_t)(chunksize - 8u);
     int64_t records = 0, last_at = -1;
-    int redo2 = 0, rounds2 = 0;
+    int batches = 0;
     uint64_t nblocks_seen = 0;
     double t_census = 0;
     ix = ppg_index{};
@@ -363,7 +407,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         J.bit_start = real[j].start;
         J.bit_limit = 8ull * (uint64_t)len;
         J.out_len = U[j];
-        J.dict_off = dict_off[j];
+        J.dict_off = (uint64_t)j * kWin;
         J.expect_end = ~0ull;
     }
     size_t b0 = 0;
@@ -371,53 +415,32 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         size_t b1 = b0 + 1;
         while (b1 < np && O[b1 + 1] - O[b0] <= cap) b1++;
         const size_t nbat = b1 - b0;
+        batches++;
         for (size_t j = b0; j < b1; j++) h2[j].out_off = O[j] - O[b0];
         HIPCHK(hipMemcpyAsync(jobs2.p + b0, h2.data() + b0, sizeof(PpgInflateJob) * nbat, hipMemcpyHostToDevice, s));
-        std::vector<uint32_t> todo(nbat);
-        for (size_t i = 0; i < nbat; i++) todo[i] = (uint32_t)(b0 + i);
+        HIPCHK(ppg_launch_inflate(s, ctx->ring_bits, ctx->lit_bits, B.comp, B.nwords, jobs2.p + b0, W.p, out.p,
+                                  res2.p + b0, (int)nbat));
+        // every piece must hand on exactly the history the next one was resolved to start with
+        std::vector<PpgGather> g(nbat);
+        for (size_t j = b0; j < b1; j++)
+            g[j - b0] = PpgGather{h2[j].out_off, (uint64_t)j * kWin, U[j], ~0ull, (uint64_t)(j + 1) * kWin};
         HIPCHK(tmp.alloc(nbat * kWin));
         HIPCHK(B.diff.alloc(nbat));
+        HIPCHK(B.gat.alloc(nbat));
+        HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * nbat, hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, tmp.p, W.p, B.diff.p, (int)nbat));
         std::vector<PpgInflateResult> r2(nbat);
         std::vector<uint32_t> hd(nbat);
-        while (!todo.empty()) {
-            rounds2++;
-            // decode (contiguous runs share a launch), then fresh tails vs the ones handed on
-            std::vector<PpgGather> g(todo.size());
-            for (size_t i = 0; i < todo.size();) {
-                size_t e = i + 1;
-                while (e < todo.size() && todo[e] == todo[e - 1] + 1) e++;
-                HIPCHK(ppg_launch_inflate(s, ctx->ring_bits, ctx->lit_bits, B.comp, B.nwords, jobs2.p + todo[i], B.tails.p,
-                                          out.p, res2.p + todo[i], (int)(e - i)));
-                i = e;
+        HIPCHK(hipMemcpyAsync(r2.data(), res2.p + b0, sizeof(PpgInflateResult) * nbat, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hd.data(), B.diff.p, 4 * nbat, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (size_t i = 0; i < nbat; i++) {
+            if (r2[i].status != PPG_OK) return r2[i].status;
+            if (r2[i].produced != U[b0 + i]) return PPG_DATA_ERROR;
+            if (hd[i]) {
+                fprintf(stderr, "ppgpu: GPU CreateIndex: piece %zu does not reproduce its resolved history\n", b0 + i);
+                return PPG_DEVICE_ERROR;
             }
-            for (size_t i = 0; i < todo.size(); i++) {
-                const uint32_t j = todo[i];
-                g[i] = PpgGather{h2[j].out_off, dict_off[j], U[j], ~0ull, (uint64_t)(real[j].slot + 1) * kWin};
-            }
-            HIPCHK(B.gat.alloc(g.size()));
-            HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
-            // fresh tail of todo[i] -> tmp[i], compared with the tail piece todo[i]+1 was given
-            HIPCHK(ppg_launch_gather(s, out.p, B.tails.p, B.gat.p, tmp.p, B.tails.p, B.diff.p, (int)todo.size()));
-            HIPCHK(hipMemcpyAsync(r2.data(), res2.p + b0, sizeof(PpgInflateResult) * nbat, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(hd.data(), B.diff.p, 4 * nbat, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            std::vector<uint32_t> next;
-            for (size_t i = 0; i < todo.size(); i++) {
-                const uint32_t j = todo[i];
-                const PpgInflateResult &r = r2[j - b0];
-                if (r.status != PPG_OK) return r.status;
-                if (r.produced != U[j]) return PPG_DATA_ERROR;
-                if (hd[i]) {
-                    // the history piece j+1 was given is stale: hand on the exact one
-                    HIPCHK(hipMemcpyAsync(B.tail_slot(real[j].slot), tmp.p + i * kWin, kWin, hipMemcpyDeviceToDevice, s));
-                    if (j + 1 < b1) next.push_back(j + 1);
-                }
-            }
-            HIPCHK(hipStreamSynchronize(s));
-            std::sort(next.begin(), next.end());
-            next.erase(std::unique(next.begin(), next.end()), next.end());
-            redo2 += (int)next.size();
-            todo.swap(next);
         }
 
         // ---- 4. '@' census of the batch's blocks and the Points among them ----
@@ -472,15 +495,15 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         }
         nblocks_seen += refs.size();
         // windows of the picked Points (zero-output Points keep the all-zero window)
-        std::vector<PpgGather> g;
+        std::vector<PpgGather> gw;
         for (const Pick &p : picks)
-            if (p.output > 0) g.push_back(PpgGather{h2[p.j].out_off, dict_off[p.j], p.rel, ~0ull, 0});
-        std::vector<uint8_t> hw(g.size() * kWin);
-        if (!g.empty()) {
-            HIPCHK(B.gat.alloc(g.size()));
-            HIPCHK(dwin.alloc(g.size() * kWin));
-            HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
-            HIPCHK(ppg_launch_gather(s, out.p, B.tails.p, B.gat.p, dwin.p, nullptr, nullptr, (int)g.size()));
+            if (p.output > 0) gw.push_back(PpgGather{h2[p.j].out_off, (uint64_t)p.j * kWin, p.rel, ~0ull, 0});
+        std::vector<uint8_t> hw(gw.size() * kWin);
+        if (!gw.empty()) {
+            HIPCHK(B.gat.alloc(gw.size()));
+            HIPCHK(dwin.alloc(gw.size() * kWin));
+            HIPCHK(hipMemcpyAsync(B.gat.p, gw.data(), sizeof(PpgGather) * gw.size(), hipMemcpyHostToDevice, s));
+            HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, dwin.p, nullptr, nullptr, (int)gw.size()));
             HIPCHK(hipMemcpyAsync(hw.data(), dwin.p, hw.size(), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
@@ -498,6 +521,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     }
     stat[3] = ms_since(t) - t_census;
     stat[4] = t_census;
+    stat[10] = (double)batches;
 
     // ---- end of the member: trailer (RFC 1952: CRC32, ISIZE) and the final Point (Core.cs:123) ----
     uint32_t nb = 0;
@@ -511,15 +535,13 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     if (last_at < 0 ? (int64_t)total > kMaxRun : (int64_t)total - 1 - last_at >= kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
     {
         std::vector<uint8_t> w(kWin);
-        HIPCHK(hipMemcpy(w.data(), B.tail_slot(real.back().slot), kWin, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(w.data(), W.p + np * kWin, kWin, hipMemcpyDeviceToHost));
         ix.add_point(0, len, (int64_t)total, 0, w.data(), nullptr, 0);
     }
     stat[5] = ms_since(t_all);
     stat[6] = (double)m;
     stat[7] = (double)np;
     stat[8] = (double)redo1;
-    stat[9] = (double)redo2;
-    stat[10] = (double)rounds2;
     stat[11] = (double)nblocks_seen;
     stat[12] = (double)ix.pts.size();
     stat[13] = (double)total;

@@ -86,6 +86,8 @@ def test_synthetic_fastq(piece, cap, device):
     gz = synth_gz(fastq_text(200_000, seed=5))
     _, st = check_both(gz, 10000, device, piece_bytes=piece, out_capacity=cap)
     assert st["real_pieces"] >= 1 and st["points"] > 10
+    if cap:
+        assert st["batches"] > 1
 
 
 def test_pigz_pieces_and_small_chunks(device):
@@ -104,8 +106,8 @@ def test_tiny_blocks_overflow_block_lists(device):
 
 
 def test_history_dependent_tails(device):
-    """data whose every later byte copies from 16 KiB back: a piece's tail depends on its
-    starting history, so the pass-1 tails are wrong and pass 2 repairs them piece by piece"""
+    """data whose every later byte copies from 16 KiB back: every piece's output is a function of
+    its starting history, resolved through the whole chain of symbolic tails"""
     rng = np.random.default_rng(11)
     r = rng.integers(0, 256, 16384, dtype=np.uint8)
     r[::200] = ord("@")
@@ -113,7 +115,7 @@ def test_history_dependent_tails(device):
     co = zlib.compressobj(6, zlib.DEFLATED, 31, 1)       # memLevel 1: 128-symbol blocks, many pieces
     gz = co.compress(data) + co.flush()
     _, st = check_both(gz, 500, device, piece_bytes=2048)
-    assert st["redo2"] > 0 and st["rounds2"] > 2
+    assert st["real_pieces"] > 5
 
 
 def test_only_stored_or_fixed_blocks(device):
