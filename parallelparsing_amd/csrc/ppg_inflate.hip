@@ -243,8 +243,13 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 // IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
 // IX = true:  CreateIndex pass 1 (ppg_index_gpu.cpp): decode whole blocks from a candidate block
 //             start until a block ends at or past stop_bit, recording every block end.
+// SGPR budget: a wave holds ceil(sgpr/16)*16 + 16 of the SIMD's 800 SGPRs, so .sgpr_count <= 80 is
+// needed for 8 waves per SIMD (97 gives 6; MI355X_MICROARCH.md, occupancy formula)
+#ifndef PPG_NUM_SGPR
+#define PPG_NUM_SGPR 80
+#endif
 template <int RB, int LBT, bool IX>
-__global__ __launch_bounds__(64) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
