@@ -35,13 +35,13 @@
 size_t ppg_inflate_lds_bytes(int ring_bits, int lit_bits);
 hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
-                              int njobs);
+                              int njobs, uint32_t *nls);
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n);
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
-                                 PpgParseInfo *info, const uint64_t *base, uint32_t *recs, int n);
+                                 PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs, int n);
 hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   const PpgParseInfo *info, const uint64_t *base, const uint32_t *recs, int64_t *keys,
@@ -372,6 +372,7 @@ struct ppg_shard {
     DevBuf<uint64_t> total;
     DevBuf<uint8_t> out;
     DevBuf<uint32_t> recs;
+    DevBuf<uint32_t> nls;      // newline census of the inflate flush (PpgInflateJob::nl_off/nl_cap)
     int64_t out_cap = 0;
     std::vector<std::pair<int32_t, int32_t>> batches;   // chunk ranges [b0, b1) relative to first
     std::vector<PpgInflateJob> h_jobs;
@@ -420,6 +421,7 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
     int64_t cap = out_capacity > 0 ? out_capacity : total_out;
     sh->h_jobs.resize((size_t)n);
     int64_t need_max = 0;
+    uint64_t nl_batch = 0, nl_need = 0;
     {
         int32_t b0 = 0;
         int64_t bbase = P[(size_t)first].output;
@@ -440,6 +442,16 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
             J.out_len = (uint64_t)ulen;
             J.dict_off = (uint64_t)i * kWin;
             J.expect_end = (size_t)first + i + 2 == P.size() ? ~0ull : (uint64_t)(8 * (to.input - base_byte) - to.bits);
+            // newline census (offsets relative to the batch, like out_off)
+            if (i == b0) nl_batch = 0;
+            const uint64_t cap = (uint64_t)ulen / kNlBytesPerEntry + 64;
+            J.nl_off = nl_batch;
+            J.nl_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFu);
+            nl_batch += J.nl_cap;
+            nl_need = std::max(nl_need, nl_batch);
+            J.raw_shift = (uint32_t)from.offset.size();
+            J.prev_byte = from.offset.empty() ? (uint32_t)'\n' : (uint32_t)from.offset.back();
+            J.pad = 0;
         }
         if (n > 0) {
             sh->batches.push_back({b0, n});
@@ -457,6 +469,18 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
         const PpgPoint &from = P[(size_t)first + i];
         horef[(size_t)i].start = hoff.size();
         horef[(size_t)i].len = (uint32_t)from.offset.size();
+        // the offset's own newlines, and whether it alone breaks R-P3 (raw[0] == '\n', "\n\n", NUL)
+        uint32_t nl = 0;
+        bool bad = false;
+        for (size_t j = 0; j < from.offset.size(); j++) {
+            const uint8_t c = from.offset[j];
+            if (c == '\n') {
+                nl++;
+                if (j == 0 || from.offset[j - 1] == '\n') bad = true;
+            }
+            if (c == 0) bad = true;
+        }
+        horef[(size_t)i].nl = nl | (bad ? PPG_OFF_SERIAL : 0u);
         hoff.insert(hoff.end(), from.offset.begin(), from.offset.end());
     }
     HIPCHK(sh->dicts.alloc((size_t)n * kWin));
@@ -476,6 +500,7 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
     // descriptor space (16 B per record) sized for >= 256-B records; a batch that needs more
     // grows it before its emit pass (ppg_shard_run)
     HIPCHK(sh->recs.alloc((size_t)(4 * (out_cap / 256 + 1024))));
+    HIPCHK(sh->nls.alloc((size_t)nl_need + 64));
     if (!sh->ev[0])
         for (auto &e : sh->ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipStreamSynchronize(s));   // the host staging vectors above die here
@@ -517,7 +542,7 @@ int ppg_shard_run(ppg_shard *sh) {
         const int nb = b1 - b0;
         HIPCHK(hipEventRecord(sh->ev[0], s));
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords, sh->jobs.p + b0,
-                                  sh->dicts.p, sh->out.p, sh->res.p + b0, nb));
+                                  sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
         HIPCHK(hipEventRecord(sh->ev[1], s));
         HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
                                       sh->info.p + b0, sh->base.p + b0, sh->total.p, nb));
@@ -527,7 +552,7 @@ int ppg_shard_run(ppg_shard *sh) {
         if ((size_t)(4 * tot) > sh->recs.n) HIPCHK(sh->recs.alloc((size_t)(4 * tot + 4096)));
         HIPCHK(hipEventRecord(sh->ev[2], s));
         HIPCHK(ppg_launch_parse_emit(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
-                                     sh->info.p + b0, sh->base.p + b0, sh->recs.p, nb));
+                                     sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p, nb));
         HIPCHK(hipEventRecord(sh->ev[3], s));
         HIPCHK(hipEventSynchronize(sh->ev[3]));
         float a = 0, b = 0, c = 0;

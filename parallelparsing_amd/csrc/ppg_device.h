@@ -15,6 +15,13 @@ struct PpgInflateJob {
     uint64_t stop_bit;
     uint32_t blk_off;
     uint32_t blk_cap;
+    // DecompressAll: the newline census fused into the output flush (ppg_inflate_kernel, nls != null).
+    // Body newline m (chunk position p) is stored as raw_shift + p at nls[nl_off + m] while m < nl_cap.
+    uint64_t nl_off;
+    uint32_t nl_cap;
+    uint32_t raw_shift;   // |offset_k|: raw index of the body's first byte
+    uint32_t prev_byte;   // raw byte before the body: offset_k's last byte, or '\n' when offset_k is empty
+    uint32_t pad;         // (raw[0] == '\n' is then an empty line, as in Parsing.Parse's view)
 };
 
 struct PpgInflateResult {
@@ -24,7 +31,12 @@ struct PpgInflateResult {
     int32_t flags;        // PPG_FLAG_*
     uint32_t nblocks;     // CreateIndex pass 1: block ends recorded
     uint32_t last;        // CreateIndex pass 1: the final block (BFINAL) was decoded
+    uint32_t newlines;    // census: '\n' bytes in the produced body
+    uint32_t pflags;      // census: PPG_PF_* below
 };
+
+#define PPG_PF_SERIAL 1     // an empty line (incl. at the offset junction) or a NUL byte in the body
+#define PPG_PF_OVERFLOW 2   // more body newlines than nl_cap: descriptors come from ppg_parse_emit
 
 // CreateIndex: one deflate block end (Core.cs:98 -- where inflate(Z_BLOCK) reports data_type & 128)
 struct PpgBlockEnd {
@@ -44,13 +56,16 @@ struct PpgAtStats {
 struct PpgOffsetRef {
     uint64_t start;
     uint32_t len;
-    uint32_t pad;
+    uint32_t nl;          // '\n' bytes in offset_k | PPG_OFF_SERIAL
 };
+
+#define PPG_OFF_SERIAL 0x80000000u   // offset_k alone has an empty line or a NUL (R-P3)
 
 struct PpgParseInfo {
     uint64_t records;     // FastqRecords emitted by Parsing.Parse for this chunk
     uint32_t newlines;    // '\n' bytes in raw
-    uint32_t serial;      // 1: parsed by the exact serial state machine
+    uint16_t serial;      // 1: parsed by the exact serial state machine
+    uint16_t emit;        // 1: census overflowed; descriptors by the ppg_parse_emit scan
 };
 
 // CreateIndex: a 32 KiB history ending at output position `end` of a piece (ppg_gather_kernel)

@@ -22,6 +22,9 @@
 
 namespace {
 constexpr int kWin = PPG_WINSIZE;
+// census capacity: one stored newline per this many output bytes (+64) per chunk; FASTQ lines
+// average well above it (150 bp Generator records: ~97 B), chunks that overflow fall back to a scan
+constexpr int kNlBytesPerEntry = 64;
 constexpr int kChunk = PPG_CHUNK;
 }
 

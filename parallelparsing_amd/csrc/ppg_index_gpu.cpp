@@ -38,7 +38,7 @@
 
 hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
-                              int njobs);
+                              int njobs, uint32_t *nls);
 hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs);
@@ -419,7 +419,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         for (size_t j = b0; j < b1; j++) h2[j].out_off = O[j] - O[b0];
         HIPCHK(hipMemcpyAsync(jobs2.p + b0, h2.data() + b0, sizeof(PpgInflateJob) * nbat, hipMemcpyHostToDevice, s));
         HIPCHK(ppg_launch_inflate(s, ctx->ring_bits, ctx->lit_bits, B.comp, B.nwords, jobs2.p + b0, W.p, out.p,
-                                  res2.p + b0, (int)nbat));
+                                  res2.p + b0, (int)nbat, nullptr));
         // every piece must hand on exactly the history the next one was resolved to start with
         std::vector<PpgGather> g(nbat);
         for (size_t j = b0; j < b1; j++)

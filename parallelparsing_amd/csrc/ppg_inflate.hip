@@ -48,6 +48,7 @@ struct __attribute__((aligned(16))) InflateLds {
     };
     uint16_t dst_sorted[32];
     uint8_t lens[320];
+    uint32_t cen[8];               // newline census: count, previous byte was '\n', PPG_PF_* flags, cap, shift, dst
 };
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
@@ -157,6 +158,129 @@ __device__ __forceinline__ void flush_range(const uint8_t *ring, uint8_t *out, u
     }
 }
 
+// ---- FASTQ newline census, fused into the output flush (DecompressAll; Parsing.cs:11-69) ----
+// Every flushed byte passes here once, in output order, as up to 16 bytes per lane (lanes in
+// increasing position, contiguous).  Per chunk it counts '\n', stores each newline's raw index
+// (the record descriptors of SURVEY A.3 R-P3 are newlines 4j..4j+3), and flags what makes the
+// 4-newline grouping differ from the serial state machine: an empty line (a '\n' right after a
+// '\n', or raw[0] == '\n') or a NUL byte.  Filler bytes ('A') pad lanes that hold fewer bytes.
+#define PPG_FILL 0x41414141u
+
+// 0x80 in every byte of x that is zero, exactly (no borrow between bytes)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
+// bit j = byte j of the 16-byte little-endian word (w0..w3) is '\n'
+__device__ __forceinline__ uint32_t nl_mask16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const uint32_t n0 = zero_bytes(w0 ^ 0x0A0A0A0Au) >> 7, n1 = zero_bytes(w1 ^ 0x0A0A0A0Au) >> 7;
+    const uint32_t n2 = zero_bytes(w2 ^ 0x0A0A0A0Au) >> 7, n3 = zero_bytes(w3 ^ 0x0A0A0A0Au) >> 7;
+    // bytes are 0/1 now: a dot product with (1,2,4,8) / (16,32,64,128) packs four of them
+    const uint32_t lo = __builtin_amdgcn_udot4(n1, 0x80402010u, __builtin_amdgcn_udot4(n0, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(n3, 0x80402010u, __builtin_amdgcn_udot4(n2, 0x08040201u, 0u, false), false);
+    return lo | (hi << 8);
+}
+
+// inclusive prefix sum over the wave (DPP row shifts + row broadcasts, GFX9 encodings)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return x;
+}
+
+struct CensusOut {
+    uint32_t *dst;          // nls + nl_off
+    uint32_t cap;           // nl_cap
+    uint32_t shift;         // raw_shift
+};
+
+// One census step: lanes [0, nact) hold bytes at chunk positions p_lane + j; `lastbit` = index of
+// a lane's last byte (15 for 16-byte lanes, 0 for single bytes); state in LDS (cen).
+__device__ __forceinline__ void census_step(uint32_t *cen, const CensusOut &co, uint32_t w0, uint32_t w1, uint32_t w2,
+                                            uint32_t w3, uint32_t p_lane, uint32_t lastbit, uint32_t nact, int lane) {
+    const uint32_t m = nl_mask16(w0, w1, w2, w3);
+    const uint32_t z = zero_bytes(w0) | zero_bytes(w1) | zero_bytes(w2) | zero_bytes(w3);
+    const uint64_t L = __ballot((m >> lastbit) & 1u);   // lanes whose last byte is '\n'
+    const uint64_t F = __ballot(m & 1u);                // lanes whose first byte is '\n'
+    const uint64_t B = __ballot((m & (m << 1)) != 0u || z != 0u);
+    uint32_t cnt = uni(cen[0]);
+    const uint32_t prevnl = uni(cen[1]);
+    uint32_t flags = uni(cen[2]);
+    if (B | (F & ((L << 1) | prevnl))) flags |= PPG_PF_SERIAL;
+    const uint32_t c = (uint32_t)__builtin_popcount(m);
+    const uint32_t incl = wave_incl_scan(c);
+    const uint32_t total = rdlane(incl, 63);
+    if (total) {
+        uint32_t idx = cnt + incl - c;
+        uint32_t mm = m;
+        while (__ballot(mm != 0u)) {
+            if (mm) {
+                const uint32_t b = (uint32_t)__builtin_ctz(mm);
+                mm &= mm - 1u;
+                if (idx < co.cap) ((__attribute__((address_space(1))) uint32_t *)co.dst)[idx] = co.shift + p_lane + b;
+                idx++;
+            }
+        }
+        cnt += total;
+        if (cnt > co.cap) flags |= PPG_PF_OVERFLOW;
+    }
+    if (lane == 0) {
+        cen[0] = cnt;
+        cen[1] = (uint32_t)(L >> (nact - 1)) & 1u;
+        cen[2] = flags;
+    }
+}
+
+__device__ __forceinline__ CensusOut census_out(const uint32_t *cen) {
+    CensusOut co;
+    co.cap = uni(cen[3]);
+    co.shift = uni(cen[4]);
+    co.dst = (uint32_t *)(((uint64_t)uni(cen[6]) << 32) | uni(cen[5]));
+    return co;
+}
+
+// flush_range + census for DecompressAll chunks: chunk positions [lo, hi) at out + out_off, as
+// steps of either aligned 16-B words (up to 1 KiB) or single bytes (an unaligned head, a tail
+// under 16 B), in output order.  One census_step per step: a single inlined instance per call
+// site.  The census parameters live in LDS (cen[3..6]), not in SGPRs the token loop keeps.
+template <int RB>
+__device__ __forceinline__ void flush_census(const uint8_t *ring, uint8_t *out, uint64_t out_off, uint32_t lo,
+                                             uint32_t hi, int lane, uint32_t *cen) {
+    constexpr uint32_t RM = (1u << RB) - 1;
+    const CensusOut co = census_out(cen);
+    for (uint32_t p = lo; p < hi;) {
+        const uint64_t g = out_off + p;
+        const uint32_t left = hi - p;
+        const uint32_t head = (uint32_t)(-g & 15);
+        uint32_t w0 = PPG_FILL, w1 = PPG_FILL, w2 = PPG_FILL, w3 = PPG_FILL, lastbit, nact;
+        if (head == 0 && left >= 16) {
+            nact = min(left / 16, 64u);
+            if ((uint32_t)lane < nact) {
+                const uint4 v = *(const uint4 *)(ring + ((uint32_t)(g + 16 * lane) & RM));
+                *(uint4 *)(out + g + 16 * lane) = v;
+                w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+            }
+            lastbit = 15;
+            nact *= 16;
+        } else {
+            nact = min(head ? head : 64u, left);
+            if ((uint32_t)lane < nact) {
+                const uint8_t c = ring[(uint32_t)(g + lane) & RM];
+                out[g + lane] = c;
+                w0 = (PPG_FILL & ~255u) | c;
+            }
+            lastbit = 0;
+        }
+        census_step(cen, co, w0, w1, w2, w3, p + (lastbit ? 16 : 1) * (uint32_t)lane, lastbit,
+                    lastbit ? nact / 16 : nact, lane);
+        p += nact;
+    }
+}
+
 // Byte at chunk position p older than the ring: the flushed output (p >= 0; this wave's own
 // earlier stores — a wave's accesses to one address are ordered) or the Point's window.  Read as
 // an aligned dword from a uniform base + 32-bit lane offset (global_load saddr form; never merged
@@ -248,12 +372,12 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 #ifndef PPG_NUM_SGPR
 #define PPG_NUM_SGPR 80
 #endif
-template <int RB, int LBT, bool IX>
+template <int RB, int LBT, bool IX, bool CEN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
-                                                         PpgBlockEnd *__restrict__ blk) {
+                                                         PpgBlockEnd *__restrict__ blk, uint32_t *__restrict__ nls) {
     constexpr uint32_t RING = 1u << RB;
     constexpr uint32_t RM = RING - 1;
     // flush unit: far references (older than REACH = RING - 64) must already be flushed; a round
@@ -281,6 +405,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #pragma unroll
         for (int q = 0; q < 4; q++) S.ring[(slot + q) & RM] = (uint8_t)(v >> (8 * q));
     }
+    constexpr bool census = CEN && !IX;
+    if (census && lane == 0) {
+        const uint64_t d = (uint64_t)(uintptr_t)(nls + J.nl_off);
+        S.cen[0] = 0;
+        S.cen[1] = J.prev_byte == '\n';
+        S.cen[2] = 0;
+        S.cen[3] = J.nl_cap;
+        S.cen[4] = J.raw_shift;
+        S.cen[5] = (uint32_t)d;
+        S.cen[6] = (uint32_t)(d >> 32);
+    }
     __syncthreads();
 
     // chunk-relative compressed stream
@@ -306,7 +441,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             const uint64_t g = out_off + (lo & IX_RING_MASK);
             flush_range<RB>(S.ring, out, g, g + (hi - lo), lane);
         } else {
-            flush_range<RB>(S.ring, out, out_off + lo, out_off + hi, lane);
+            if constexpr (census) {
+                flush_census<RB>(S.ring, out, out_off, lo, hi, lane, S.cen);
+            } else {
+                flush_range<RB>(S.ring, out, out_off + lo, out_off + hi, lane);
+            }
         }
     };
     uint32_t nblk = 0;
@@ -600,6 +739,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         res[k].flags = flags;
         res[k].nblocks = nblk;
         res[k].last = (uint32_t)last;
+        res[k].newlines = census ? S.cen[0] : 0;
+        res[k].pflags = census ? S.cen[2] : 0;
     }
 }
 
@@ -618,12 +759,16 @@ size_t ppg_inflate_lds_bytes(int ring_bits, int lit_bits) {
 
 hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
-                              int njobs) {
+                              int njobs, uint32_t *nls) {
     if (njobs <= 0) return hipSuccess;
 #define X(R, L)                                                                                               \
     if (ring_bits == R && lit_bits == L) {                                                                    \
-        hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false>), dim3(njobs), dim3(64), sizeof(InflateLds<R, L>), s, \
-                           comp, nwords, jobs, dicts, out, res, njobs, nullptr);                             \
+        if (nls)                                                                                              \
+            hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, true>), dim3(njobs), dim3(64),                \
+                               sizeof(InflateLds<R, L>), s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls); \
+        else                                                                                                  \
+            hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, false>), dim3(njobs), dim3(64),               \
+                               sizeof(InflateLds<R, L>), s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls); \
         return hipGetLastError();                                                                             \
     }
     PPG_VARIANTS(X)
@@ -636,7 +781,7 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs) {
     if (njobs <= 0) return hipSuccess;
-    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true>), dim3(njobs), dim3(64), sizeof(InflateLds<10, 8>), s, comp,
-                       nwords, jobs, dicts, out, res, njobs, blk);
+    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64), sizeof(InflateLds<10, 8>), s, comp,
+                       nwords, jobs, dicts, out, res, njobs, blk, nullptr);
     return hipGetLastError();
 }

@@ -1,11 +1,12 @@
 // ppg_parse.hip — gfx950 kernels for the FASTQ record scan of the DecompressAll path
 // (Decompressor/Parsing.cs:11-69 over raw_k = offset_k ++ chunk_k).
 //
-//   ppg_parse_count   per-chunk newline census + the conditions under which "record j = newlines
-//                     4j..4j+3" equals the serial state machine (R-P3)
+//   ppg_parse_finish  per-chunk record counts from the newline census fused into the inflate
+//                     flush, + whether "record j = newlines 4j..4j+3" equals the serial machine (R-P3)
+//   ppg_parse_place   per-record descriptors (n1..n4) from the census's stored newline positions
 //   ppg_parse_serial  the exact Parsing.Parse state machine for chunks the census declines
 //   ppg_scan_counts   exclusive scan of per-chunk record counts -> record bases
-//   ppg_parse_emit    per-record descriptors (n1..n4 newline positions) for fast chunks
+//   ppg_parse_emit    descriptors by scanning the body (chunks whose census overflowed nl_cap)
 //   ppg_record_keys   per-record spot ("major") number from the identifier line, for pairing
 //                     the two files of a read pair
 #include <hip/hip_runtime.h>
@@ -22,61 +23,26 @@ __device__ __forceinline__ uint8_t raw_at(const uint8_t *off, uint32_t off_len, 
     return i < blen ? body[i] : (uint8_t)0;
 }
 
-// Newline census: per chunk the '\n' count and whether the 4-newline grouping could differ
-// from Parsing.Parse: an empty line anywhere ("\n\n" or raw[0]=='\n'), or a '\0' byte.  Those
-// chunks go to ppg_parse_serial.  256 threads per chunk, 16 B per thread per 4 KiB tile.
-extern "C" __global__ __launch_bounds__(256) void ppg_parse_count(
-    const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
-    const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, PpgParseInfo *__restrict__ info, int nchunks) {
-    const int k = blockIdx.x;
+// Per-chunk record counts from the newline census that ppg_inflate_kernel fused into its output
+// flush: raw_k = offset_k ++ body_k has off_nl + body_nl newlines; "record j = newlines 4j..4j+3"
+// equals the serial state machine unless raw_k has an empty line or a NUL (R-P3) -- those chunks
+// go to ppg_parse_serial.  One thread per chunk.
+extern "C" __global__ __launch_bounds__(256) void ppg_parse_finish(const PpgInflateResult *__restrict__ ires,
+                                                                   const PpgOffsetRef *__restrict__ oref,
+                                                                   PpgParseInfo *__restrict__ info, int nchunks) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= nchunks) return;
-    const int t = threadIdx.x;
-    __shared__ uint32_t red_nl[4], red_flag[4];
-    const uint64_t g0 = jobs[k].out_off;
-    const uint64_t blen = ires[k].status == 0 ? ires[k].produced : 0;
-    const uint8_t *off = offs + oref[k].start;
-    const uint32_t olen = oref[k].len;
-    uint32_t nl = 0, flag = 0;
-    // offset prefix (short): byte-wise; pair check spans into the body's first byte
-    for (uint32_t i = t; i < olen; i += 256) {
-        uint8_t c = off[i];
-        uint8_t p = i ? off[i - 1] : (uint8_t)0;
-        if (c == '\n') { nl++; if (i == 0 || p == '\n') flag = 1; }
-        if (c == 0) flag = 1;
-    }
-    // body: 16-B aligned words over [g0, g0+blen)
-    const uint64_t g1 = g0 + blen;
-    const uint64_t a0 = g0 & ~15ull;
-    for (uint64_t w = a0 + (uint64_t)t * 16; w < g1; w += 4096) {
-        uint4 v = *(const uint4 *)(out + w);
-        uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-        // previous byte in raw order: out[g-1] inside the body; at g0 the last offset byte, or
-        // "raw start" (a leading '\n' is itself an empty line) when the offset is empty
-        uint8_t prev = w > g0 ? out[w - 1] : (uint8_t)0;
-        const uint8_t at_g0 = olen ? off[olen - 1] : (uint8_t)'\n';
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            uint8_t c = (uint8_t)(wd[q >> 2] >> (8 * (q & 3)));
-            uint64_t g = w + q;
-            uint8_t p = g == g0 ? at_g0 : prev;
-            if (g >= g0 && g < g1) {
-                if (c == '\n') { nl++; if (p == '\n') flag = 1; }
-                if (c == 0) flag = 1;
-            }
-            prev = c;
-        }
-    }
-    // reduce over 256 threads (4 waves)
-    for (int o = 32; o > 0; o >>= 1) { nl += __shfl_down(nl, o); flag |= __shfl_down(flag, o); }
-    if ((t & 63) == 0) { red_nl[t >> 6] = nl; red_flag[t >> 6] = flag; }
-    __syncthreads();
-    if (t == 0) {
-        uint32_t n = red_nl[0] + red_nl[1] + red_nl[2] + red_nl[3];
-        uint32_t f = red_flag[0] | red_flag[1] | red_flag[2] | red_flag[3];
-        info[k].newlines = n;
-        info[k].serial = f;
-        info[k].records = (ires[k].status == 0 && !f) ? n / 4 : 0;
-    }
+    const PpgInflateResult r = ires[k];
+    const uint32_t onl = oref[k].nl & ~PPG_OFF_SERIAL;
+    const bool ok = r.status == 0;
+    const bool serial = (oref[k].nl & PPG_OFF_SERIAL) || (r.pflags & PPG_PF_SERIAL);
+    const uint32_t nl = onl + (ok ? r.newlines : 0);
+    PpgParseInfo f;
+    f.newlines = nl;
+    f.serial = serial ? 1 : 0;
+    f.emit = ok && !serial && (r.pflags & PPG_PF_OVERFLOW) ? 1 : 0;
+    f.records = ok && !serial ? nl / 4 : 0;
+    info[k] = f;
 }
 
 // Parsing.Parse (Parsing.cs:11-69) exactly, one lane per chunk that the census declined.
@@ -146,14 +112,15 @@ extern "C" __global__ __launch_bounds__(1024) void ppg_scan_counts(const PpgPars
     if (t == 1023) *total = part[1023];
 }
 
-// Descriptors for fast-path chunks: newline m (m < 4*records) is field m%4 of record m/4.
+// Descriptors of fast-path chunks whose census overflowed nl_cap: a scan of the body for its
+// newlines.  Newline m (m < 4*records) is field m%4 of record m/4.
 extern "C" __global__ __launch_bounds__(256) void ppg_parse_emit(
     const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
     const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, const PpgParseInfo *__restrict__ info,
     const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks) {
     const int k = blockIdx.x;
     if (k >= nchunks) return;
-    if (info[k].serial || ires[k].status != 0) return;
+    if (!info[k].emit || info[k].serial || ires[k].status != 0) return;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     __shared__ uint32_t wsum[4];
     const uint64_t nrec = info[k].records;
@@ -213,6 +180,32 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_emit(
     }
 }
 
+// Descriptors of fast-path chunks from the census: the offset's newlines (a few hundred bytes,
+// scanned here) then the body's, already stored as raw indices by the inflate kernel; newline m
+// (m < 4*records) is field m%4 of record m/4.  One block per chunk; a copy, not a scan.
+extern "C" __global__ __launch_bounds__(256) void ppg_parse_place(
+    const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires, const uint8_t *__restrict__ offs,
+    const PpgOffsetRef *__restrict__ oref, const PpgParseInfo *__restrict__ info, const uint64_t *__restrict__ base,
+    const uint32_t *__restrict__ nls, uint32_t *__restrict__ recs, int nchunks) {
+    const int k = blockIdx.x;
+    if (k >= nchunks) return;
+    const PpgParseInfo f = info[k];
+    if (f.serial || f.emit || ires[k].status != 0 || f.records == 0) return;
+    const uint64_t limit = 4 * f.records;
+    uint32_t *dst = recs + 4 * base[k];
+    const uint32_t onl = oref[k].nl & ~PPG_OFF_SERIAL;
+    if (onl && threadIdx.x == 0) {
+        const uint8_t *off = offs + oref[k].start;
+        uint64_t m = 0;
+        for (uint32_t i = 0, n = oref[k].len; i < n && m < limit; i++)
+            if (off[i] == '\n') dst[m++] = i;
+    }
+    if (limit <= onl) return;
+    const uint64_t cnt = min(limit - onl, (uint64_t)ires[k].newlines);
+    const uint32_t *src = nls + jobs[k].nl_off;
+    for (uint64_t i = threadIdx.x; i < cnt; i += 256) dst[onl + i] = src[i];
+}
+
 // Spot number of every record: Identifier = raw[start+1, n1) ("SRR<id>.<major>.<minor> ..."):
 // the digits between its first and second '.'; -1 when the identifier has no such field.  The
 // first record of a chunk that lies wholly inside offset_k is the previous chunk's last record
@@ -258,21 +251,24 @@ extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
 // ------------------------------------------------------------------------------------------
 // Host-side launchers (called from ppg_api.cpp).
 // ------------------------------------------------------------------------------------------
+// after the inflate launch: per-chunk counts (census, or the serial machine) and their scan
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_parse_count, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, n);
+    hipLaunchKernelGGL(ppg_parse_finish, dim3((n + 255) / 256), dim3(256), 0, s, ires, oref, info, n);
     hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info,
                        (const uint64_t *)nullptr, (uint32_t *)nullptr, n, 0);
     hipLaunchKernelGGL(ppg_scan_counts, dim3(1), dim3(1024), 0, s, info, base, total, n);
     return hipGetLastError();
 }
 
+// descriptors: census copy (most chunks), body scan (census overflow), serial machine (R-P3 fails)
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
-                                 PpgParseInfo *info, const uint64_t *base, uint32_t *recs, int n) {
+                                 PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs, int n) {
     if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_parse_place, dim3(n), dim3(256), 0, s, jobs, ires, offs, oref, info, base, nls, recs, n);
     hipLaunchKernelGGL(ppg_parse_emit, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, n);
     hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, 1);
     return hipGetLastError();
