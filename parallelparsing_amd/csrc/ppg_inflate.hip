@@ -571,18 +571,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         fl_next = uni(fl_next);
 
         // ---- token rounds ----
+        // A round emits at most 64 output bytes.  A match crossing that boundary is carried: its
+        // remaining bytes open the next round as a token at output offset 0.  Rounds are software
+        // pipelined: round i+1 is decoded (stream + tables + walk: no output bytes needed) while
+        // round i's source bytes are in flight — references older than the LDS ring come from
+        // HBM/L2/MALL (far_byte), and the next round's decode hides that latency.
         uint32_t bp = rd_pos(r);
         uint32_t cn = 0, cw = 0;   // carried: bytes left of the last round's last match, its token word
-        while (pos < len) {
-            // A round emits at most 64 output bytes.  A match crossing that boundary is carried:
-            // its remaining bytes open the next round as a token at output offset 0.
+
+        // decode of the round starting at output position pos, stream bit bp, carry (cn, cw):
+        // returns the token words placed at their output offsets, the output bytes the round's
+        // tokens cover (off), the bit advance (adv) and whether it stopped at a special token
+        struct Round { uint32_t vtin, off, adv; bool spec; };
+        auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos) -> Round {
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t vtin = 0;
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
             bool spec = false;
             if (off < min(64u, len - pos)) {
-                // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS ring)
-                st_enter(r, S.stream, bp >> 10, lane);
+                // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
+                // ring; st_enter already made the segment resident)
                 const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
                 const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
                 const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2], x3 = sw[3], x4 = sw[4];
@@ -636,51 +644,111 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 spec = s == 255u;
                 s = half + (spec ? ((t >> 17) & 63u) : s);   // bit offset of the next token
             }
-            const uint32_t tot = min(off, len - pos);    // output bytes of the round's tokens
-            const uint32_t rout = min(tot, 64u);         // ... emitted this round
-            const uint64_t mo = __ballot(vtin != 0);     // token start offsets (never 0 words)
+            return Round{vtin, off, s, spec};
+        };
 
-            // ---- emit the round's output bytes, one per lane ----
-            // All 64 lanes write: lanes past rout leave garbage in the slots of positions
-            // [pos + rout, pos + 64), which later rounds overwrite before use; the slots' previous
-            // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
-            // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
-            {
-                const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
-                const uint32_t inf = bperm(sj << 2, vtin);
-                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
-                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-                if (jj < -(int32_t)(RING - 64))                       // far (literals: jj >= -512)
-                    val = far_byte<IX>(ob, oa, dict, (int32_t)pos + jj);
-                const bool dep = jj >= 0;                             // produced in this round
-                if (__ballot(dep)) {
-                    // chains inside the round (short distances): pointer doubling to a resolved byte
-                    int32_t ptr = dep ? jj : lane;
-                    for (;;) {
-                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
-                        if (!__ballot(p2 != ptr)) break;
-                        ptr = p2;
+        bool block_done = false;
+        while (!block_done) {
+            // pipelined rounds until a special token, the output limit or (IX) a runaway
+            st_enter(r, S.stream, bp >> 10, lane);
+            // The finish runs on every iteration (so no vmcnt wait is left for the issue to
+            // inherit); the first one commits a dummy round of zero bytes at pos, harmlessly: the
+            // slots of [pos, pos + 64) hold positions older than REACH and already flushed, and the
+            // first real round overwrites them before they are read.
+            bool stop = false, spec = false;
+            uint32_t p_pos = pos;   // output position of the pending round
+            uint32_t p_val = 0;     // pending round: this lane's byte (or its in-flight far load)
+            int32_t p_jj = -1;      // pending round: this lane's source, relative to the round
+            for (;;) {
+                const bool dec = !stop && pos < len;
+                Round R{0, 0, 0, false};
+                if (dec) R = decode(bp, cn, cw, pos);
+                {
+                    // ---- finish the pending round: in-round chains, then one byte per lane ----
+                    // All 64 lanes write: lanes past the round's bytes leave garbage in the slots of
+                    // positions [p_pos + rout, p_pos + 64), which later rounds overwrite before use;
+                    // the slots' previous bytes are therefore never read from the ring — references
+                    // reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
+                    uint32_t val = p_val;
+                    if (p_jj < -(1 << 30)) val = (val >> (p_jj & 31)) & 255u;   // a far byte
+                    const bool dep = p_jj >= 0;                       // produced in this round
+                    if (__ballot(dep)) {
+                        // chains inside the round (short distances): pointer doubling to a resolved byte
+                        int32_t ptr = dep ? p_jj : lane;
+                        for (;;) {
+                            const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
+                            if (!__ballot(p2 != ptr)) break;
+                            ptr = p2;
+                        }
+                        val = bperm((uint32_t)ptr << 2, val);
                     }
-                    val = bperm((uint32_t)ptr << 2, val);
+                    S.ring[(rb0 + p_pos + lane) & RM] = (uint8_t)val;
+                    if (pos >= fl_next) {
+                        flush(fl_done, fl_next);
+                        fl_done = fl_next;
+                        fl_next += UNIT;
+                    }
                 }
-                S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
+                if (!dec) break;
+                const uint32_t tot = min(R.off, len - pos);   // output bytes of the round's tokens
+                const uint32_t rout = min(tot, 64u);          // ... emitted this round
+                const uint64_t mo = __ballot(R.vtin != 0);    // token start offsets (never 0 words)
+                spec = R.spec;
+                // the next round's stream segment, before this round's far loads are issued (its
+                // s_waitcnt then does not wait for them)
+                stop = spec || pos + rout >= len;
+                if constexpr (IX) {   // past the member, or runaway output (a false start)
+                    if (bp + R.adv > bit_limit || pos + rout > 0xF0000000u) { status = ST_DATA_ERROR; stop = true; }
+                }
+                if (!stop) st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+                // ---- issue the round's source bytes, one per lane ----
+                {
+                    const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
+                    const uint32_t inf = bperm(sj << 2, R.vtin);
+                    const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
+                    const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                    uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                    int32_t pj = jj;
+                    if (jj < -(int32_t)(RING - 64)) {                     // far (literals: jj >= -512)
+                        // issue only: the raw word lands in val, the byte is extracted at the finish
+                        // (pj = INT_MIN | shift marks it), so nothing here waits for the load
+                        const int32_t p = (int32_t)pos + jj;
+                        if (p >= 0) {
+                            const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
+                            val = *(const uint32_t *)(ob + (q & ~3u));
+                            pj = (int32_t)(0x80000000u | (8 * (q & 3)));
+                        } else {
+                            val = dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
+                            pj = (int32_t)0x80000000u;
+                        }
+                    }
+#if defined(PPG_PAD_VALU) || defined(PPG_PAD_SALU)
+                    {   // issue-bound probe (A/B only): extra independent VALU or SALU per round
+                        uint32_t pv = (uint32_t)lane, ps = pos;
+#ifdef PPG_PAD_VALU
+#pragma unroll
+                        for (int q = 0; q < PPG_PAD_VALU; q++) asm volatile("v_mov_b32 %0, %0" : "+v"(pv));
+#endif
+#ifdef PPG_PAD_SALU
+#pragma unroll
+                        for (int q = 0; q < PPG_PAD_SALU; q++) asm volatile("s_mov_b32 %0, %0" : "+s"(ps));
+#endif
+                        val += (pv ^ (uint32_t)lane) + (ps ^ pos);
+                    }
+#endif
+                    p_val = val;
+                    p_jj = pj;
+                    p_pos = pos;
+                }
+                cn = tot - rout;
+                if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
+                    cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
+                }
+                pos += rout;
+                bp += R.adv;
             }
-            cn = tot - rout;
-            if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
-                cw = rdlane(vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
-            }
-            pos += rout;
-            if (pos >= fl_next) {
-                flush(fl_done, fl_next);
-                fl_done = fl_next;
-                fl_next += UNIT;
-            }
-            bp += s;
-            if constexpr (IX) {   // past the member, or runaway output (a false start)
-                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
-            }
-            if (!spec) continue;
+            if (status != ST_OK) break;
+            if (!spec || pos >= len) break;
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
             rd_seek(r, S.stream, bp, lane);
@@ -693,7 +761,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             } else if (sym == 256) {
                 in_block = 0;
                 bp = rd_pos(r);
-                break;
+                block_done = true;
             } else {
                 const uint32_t ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
                 rd_refill(r, S.stream, lane);
@@ -704,12 +772,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 copy_match<RB, IX>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
             }
-            bp = rd_pos(r);
+            if (!block_done) bp = rd_pos(r);
             if (pos >= fl_next) {
                 flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
+            if (pos >= len) break;
         }
         if (status != ST_OK) break;
         rd_seek(r, S.stream, bp, lane);   // the next block header / the R-E5 check read from bp
