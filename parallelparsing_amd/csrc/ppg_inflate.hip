@@ -336,12 +336,14 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uin
 }
 
 // One speculative token from the 64 stream bits (lo, hi) at some bit offset, decoded with the
-// root tables.  Token word: [7:0] index of the next token's bit offset (this lane + its bits),
-// [16:8] output bytes (1: literal), [31:17] distance - 1 (match) or 0x100 | byte (literal: then
-// lane - 1 - field lies in [-512, -194]: negative and, for any ring >= 1 KiB, never "far", see
-// the emit).  A special token (a code the root tables do not resolve: end-of-block, invalid,
-// long) is 255 | (0x100 | lane) << 17: next
-// index 255 ends the walk, 0 bytes.  Never 0 (the emit finds tokens by that).
+// root tables.  Token word: [7:0] the token's bits, [16:8] output bytes (1: literal), [31:17]
+// distance - 1 (match) or 0x100 | byte (literal: then lane - 1 - field lies in [-512, -194]:
+// negative and, for any ring >= 1 KiB, never "far", see the emit).  The walk adds whole words to
+// its state (see Round), so [7:0] and [16:8] must not carry into each other: bits <= 48, bytes <= 258.
+// A special token (a code the root tables do not resolve: end-of-block, invalid, long) is
+// 128 | 0x100 << 17: bits 128 set bit 7 of the walk's candidate index, which ends the walk; 0
+// bytes; the field keeps the emit's source for lanes past it negative and near.  Never 0 (the
+// emit finds tokens by that).
 template <int LBT>
 __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32_t *dst, uint32_t lo, uint32_t hi,
                                                uint32_t lane) {
@@ -359,9 +361,8 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     const uint32_t nb = ((mlen - 1) & lm) + 1;                      // output bytes
     const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
     const uint32_t field = ((dist - 1) & lm) | ((0x100u | (e >> 16)) & ~lm);
-    const uint32_t tok = (lane + tb) | (nb << 8) | (field << 17);
-    const uint32_t spec = 255u | ((0x100u | lane) << 17);
-    return (tok & ~sm) | (spec & sm);
+    const uint32_t tok = tb | (nb << 8) | (field << 17);
+    return (tok & ~sm) | ((128u | (0x100u << 17)) & sm);
 }
 
 // IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
@@ -601,48 +602,55 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                                                      __builtin_amdgcn_alignbit(x4, x3, o), (uint32_t)lane);
 
                 // ---- walk the real token chain (wave-uniform): offset s -> s + bits(s) ----
-                // Each token goes to the lane of its output offset (vtin).  The walk runs through
+                // Each token goes to the lane of its output offset (vtin).  The walk state is one
+                // SGPR, X = s | off << 8 (+ carry-free garbage above bit 16 from the fields): a token
+                // word adds its bits to s and its bytes to off in one s_add, and v_readlane /
+                // v_writelane use only bits [5:0] of their lane select (checked on gfx950), so
+                // X itself selects candidate s and X >> 8 output offset off.  The walk runs through
                 // the first 64 offsets (vta), then the next 64 (vtb), and stops at a special token
-                // (recorded with 0 bytes, harmlessly), past the span, or once no further token can
-                // start inside the round's first min(64, len - pos) output bytes.
+                // (recorded with 0 bytes, harmlessly; s gains 128), past the span, or once no
+                // further token can start inside the round's first min(64, len - pos) output bytes.
+                // Per token: 2 VALU, 3 SALU, 1 branch.
+                constexpr uint32_t STOP = 0x1C0C0u;   // s >= 64 (bits 7:6) or off >= 64 (bits 16:14)
+                uint32_t X;
                 if (len - pos >= 64) {
+                    X = off << 8;
                     do {
-                        t = rdlane(vta, s);
-                        vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                        off += (t >> 8) & 511u;
-                        s = t & 255u;
-                    } while ((s | off) < 64u);
-                    if (off < 64 && s != 255u) {   // crossed into the second 64 offsets
-                        s -= 64;
+                        t = rdlane(vta, X);
+                        vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
+                        X += t;
+                    } while ((X & STOP) == 0u);
+                    if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
+                        X -= 64;
                         half = 64;
                         do {
-                            t = rdlane(vtb, s);
-                            vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                            off += (t >> 8) & 511u;
-                            s = t & 255u;
-                        } while ((s | off) < 64u);
+                            t = rdlane(vtb, X);
+                            vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
+                            X += t;
+                        } while ((X & STOP) == 0u);
                     }
+                    off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
+                    X = (off + cl) << 8;
                     do {
-                        t = rdlane(vta, s);
-                        vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                        off += (t >> 8) & 511u;
-                        s = t & 255u;
-                    } while (max(s, off + cl) < 64u);
-                    if (off + cl < 64 && s != 255u) {
-                        s -= 64;
+                        t = rdlane(vta, X);
+                        vtin = (uint32_t)llvm_writelane((int)t, (int)((X >> 8) - cl), (int)vtin);
+                        X += t;
+                    } while ((X & STOP) == 0u);
+                    if ((X & (STOP & ~0x40u)) == 0u) {
+                        X -= 64;
                         half = 64;
                         do {
-                            t = rdlane(vtb, s);
-                            vtin = (uint32_t)llvm_writelane((int)t, (int)off, (int)vtin);
-                            off += (t >> 8) & 511u;
-                            s = t & 255u;
-                        } while (max(s, off + cl) < 64u);
+                            t = rdlane(vtb, X);
+                            vtin = (uint32_t)llvm_writelane((int)t, (int)((X >> 8) - cl), (int)vtin);
+                            X += t;
+                        } while ((X & STOP) == 0u);
                     }
+                    off = ((X >> 8) & 511u) - cl;
                 }
-                spec = s == 255u;
-                s = half + (spec ? ((t >> 17) & 63u) : s);   // bit offset of the next token
+                spec = (X & 128u) != 0u;
+                s = half + (X & 127u);   // bit offset of the next token (of the special one: bit 7 dropped)
             }
             return Round{vtin, off, s, spec};
         };
