@@ -422,6 +422,10 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
     sh->h_jobs.resize((size_t)n);
     int64_t need_max = 0;
     uint64_t nl_batch = 0, nl_need = 0;
+    // census capacity: one stored newline per kNlBytesPerEntry output bytes; PPG_NL_BYTES overrides
+    // (tests force the overflow fallback with a huge value)
+    uint64_t nl_bytes = kNlBytesPerEntry;
+    if (const char *e = getenv("PPG_NL_BYTES")) nl_bytes = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     {
         int32_t b0 = 0;
         int64_t bbase = P[(size_t)first].output;
@@ -444,7 +448,7 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
             J.expect_end = (size_t)first + i + 2 == P.size() ? ~0ull : (uint64_t)(8 * (to.input - base_byte) - to.bits);
             // newline census (offsets relative to the batch, like out_off)
             if (i == b0) nl_batch = 0;
-            const uint64_t cap = (uint64_t)ulen / kNlBytesPerEntry + 64;
+            const uint64_t cap = nl_bytes >= (1ull << 40) ? 0 : (uint64_t)ulen / nl_bytes + 64;
             J.nl_off = nl_batch;
             J.nl_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFu);
             nl_batch += J.nl_cap;

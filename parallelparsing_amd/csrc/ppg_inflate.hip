@@ -573,10 +573,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 
         // ---- token rounds ----
         // A round emits at most 64 output bytes.  A match crossing that boundary is carried: its
-        // remaining bytes open the next round as a token at output offset 0.  Rounds are software
-        // pipelined: round i+1 is decoded (stream + tables + walk: no output bytes needed) while
-        // round i's source bytes are in flight — references older than the LDS ring come from
-        // HBM/L2/MALL (far_byte), and the next round's decode hides that latency.
+        // remaining bytes open the next round as a token at output offset 0.  (Software pipelining
+        // the next round's decode over this round's far loads measured no gain: at 8 waves per
+        // SIMD the kernel is issue-bound, chiefly on SALU — see DESIGN.md.)
         uint32_t bp = rd_pos(r);
         uint32_t cn = 0, cw = 0;   // carried: bytes left of the last round's last match, its token word
 
@@ -655,108 +654,83 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             return Round{vtin, off, s, spec};
         };
 
-        bool block_done = false;
-        while (!block_done) {
-            // pipelined rounds until a special token, the output limit or (IX) a runaway
+        for (;;) {
+            // ---- one round: decode + walk, then one output byte per lane ----
             st_enter(r, S.stream, bp >> 10, lane);
-            // The finish runs on every iteration (so no vmcnt wait is left for the issue to
-            // inherit); the first one commits a dummy round of zero bytes at pos, harmlessly: the
-            // slots of [pos, pos + 64) hold positions older than REACH and already flushed, and the
-            // first real round overwrites them before they are read.
-            bool stop = false, spec = false;
-            uint32_t p_pos = pos;   // output position of the pending round
-            uint32_t p_val = 0;     // pending round: this lane's byte (or its in-flight far load)
-            int32_t p_jj = -1;      // pending round: this lane's source, relative to the round
-            for (;;) {
-                const bool dec = !stop && pos < len;
-                Round R{0, 0, 0, false};
-                if (dec) R = decode(bp, cn, cw, pos);
-                {
-                    // ---- finish the pending round: in-round chains, then one byte per lane ----
-                    // All 64 lanes write: lanes past the round's bytes leave garbage in the slots of
-                    // positions [p_pos + rout, p_pos + 64), which later rounds overwrite before use;
-                    // the slots' previous bytes are therefore never read from the ring — references
-                    // reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
-                    uint32_t val = p_val;
-                    if (p_jj < -(1 << 30)) val = (val >> (p_jj & 31)) & 255u;   // a far byte
-                    const bool dep = p_jj >= 0;                       // produced in this round
-                    if (__ballot(dep)) {
-                        // chains inside the round (short distances): pointer doubling to a resolved byte
-                        int32_t ptr = dep ? p_jj : lane;
-                        for (;;) {
-                            const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
-                            if (!__ballot(p2 != ptr)) break;
-                            ptr = p2;
-                        }
-                        val = bperm((uint32_t)ptr << 2, val);
-                    }
-                    S.ring[(rb0 + p_pos + lane) & RM] = (uint8_t)val;
-                    if (pos >= fl_next) {
-                        flush(fl_done, fl_next);
-                        fl_done = fl_next;
-                        fl_next += UNIT;
+            const Round R = decode(bp, cn, cw, pos);
+            const uint32_t tot = min(R.off, len - pos);   // output bytes of the round's tokens
+            const uint32_t rout = min(tot, 64u);          // ... emitted this round
+            const uint64_t mo = __ballot(R.vtin != 0);    // token start offsets (never 0 words)
+            // All 64 lanes write: lanes past rout leave garbage in the slots of positions
+            // [pos + rout, pos + 64), which later rounds overwrite before use; the slots' previous
+            // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
+            // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
+            {
+                const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
+                const uint32_t inf = bperm(sj << 2, R.vtin);
+                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
+                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
+                const uint64_t fm = __ballot(far);
+                if (fm) {
+                    // older than the ring: the flushed output (this wave's own earlier stores), as
+                    // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
+                    // juggling); references into the Point's window (first 32 KiB only) separately
+                    const int32_t p = (int32_t)pos + jj;
+                    const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
+                    const bool fo = far && p >= 0;
+                    const uint32_t w = *(const uint32_t *)(ob + (fo ? (q & ~3u) : 0u));
+                    if (fo) val = (w >> (8 * (q & 3))) & 255u;
+                    if (__ballot(far && p < 0)) {
+                        if (far && p < 0) val = dict[32768u + (uint32_t)p];   // p >= -32768
                     }
                 }
-                if (!dec) break;
-                const uint32_t tot = min(R.off, len - pos);   // output bytes of the round's tokens
-                const uint32_t rout = min(tot, 64u);          // ... emitted this round
-                const uint64_t mo = __ballot(R.vtin != 0);    // token start offsets (never 0 words)
-                spec = R.spec;
-                // the next round's stream segment, before this round's far loads are issued (its
-                // s_waitcnt then does not wait for them)
-                stop = spec || pos + rout >= len;
-                if constexpr (IX) {   // past the member, or runaway output (a false start)
-                    if (bp + R.adv > bit_limit || pos + rout > 0xF0000000u) { status = ST_DATA_ERROR; stop = true; }
-                }
-                if (!stop) st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
-                // ---- issue the round's source bytes, one per lane ----
-                {
-                    const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
-                    const uint32_t inf = bperm(sj << 2, R.vtin);
-                    const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
-                    const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                    uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-                    int32_t pj = jj;
-                    if (jj < -(int32_t)(RING - 64)) {                     // far (literals: jj >= -512)
-                        // issue only: the raw word lands in val, the byte is extracted at the finish
-                        // (pj = INT_MIN | shift marks it), so nothing here waits for the load
-                        const int32_t p = (int32_t)pos + jj;
-                        if (p >= 0) {
-                            const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
-                            val = *(const uint32_t *)(ob + (q & ~3u));
-                            pj = (int32_t)(0x80000000u | (8 * (q & 3)));
-                        } else {
-                            val = dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
-                            pj = (int32_t)0x80000000u;
-                        }
+                const bool dep = jj >= 0;                             // produced in this round
+                if (__ballot(dep)) {
+                    // chains inside the round (short distances): pointer doubling to a resolved byte
+                    int32_t ptr = dep ? jj : lane;
+                    for (;;) {
+                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
+                        if (!__ballot(p2 != ptr)) break;
+                        ptr = p2;
                     }
+                    val = bperm((uint32_t)ptr << 2, val);
+                }
 #if defined(PPG_PAD_VALU) || defined(PPG_PAD_SALU)
-                    {   // issue-bound probe (A/B only): extra independent VALU or SALU per round
-                        uint32_t pv = (uint32_t)lane, ps = pos;
+                {   // issue-bound probe (A/B only): extra independent VALU or SALU per round
+                    uint32_t pv = (uint32_t)lane, ps = pos;
 #ifdef PPG_PAD_VALU
 #pragma unroll
-                        for (int q = 0; q < PPG_PAD_VALU; q++) asm volatile("v_mov_b32 %0, %0" : "+v"(pv));
+                    for (int q = 0; q < PPG_PAD_VALU; q++) asm volatile("v_mov_b32 %0, %0" : "+v"(pv));
 #endif
 #ifdef PPG_PAD_SALU
 #pragma unroll
-                        for (int q = 0; q < PPG_PAD_SALU; q++) asm volatile("s_mov_b32 %0, %0" : "+s"(ps));
+                    for (int q = 0; q < PPG_PAD_SALU; q++) asm volatile("s_mov_b32 %0, %0" : "+s"(ps));
 #endif
-                        val += (pv ^ (uint32_t)lane) + (ps ^ pos);
-                    }
+                    val += (pv ^ (uint32_t)lane) + (ps ^ pos);
+                }
 #endif
-                    p_val = val;
-                    p_jj = pj;
-                    p_pos = pos;
-                }
-                cn = tot - rout;
-                if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
-                    cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
-                }
-                pos += rout;
-                bp += R.adv;
+                S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
             }
-            if (status != ST_OK) break;
-            if (!spec || pos >= len) break;
+            cn = tot - rout;
+            if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
+                cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
+            }
+            pos += rout;
+            if (pos >= fl_next) {
+                flush(fl_done, fl_next);
+                fl_done = fl_next;
+                fl_next += UNIT;
+            }
+            bp += R.adv;
+            if constexpr (IX) {   // past the member, or runaway output (a false start)
+                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
+            }
+            if (!R.spec) {
+                if (pos < len) continue;
+                break;
+            }
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
             rd_seek(r, S.stream, bp, lane);
@@ -769,7 +743,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             } else if (sym == 256) {
                 in_block = 0;
                 bp = rd_pos(r);
-                block_done = true;
+                break;
             } else {
                 const uint32_t ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
                 rd_refill(r, S.stream, lane);
@@ -780,7 +754,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 copy_match<RB, IX>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
             }
-            if (!block_done) bp = rd_pos(r);
+            bp = rd_pos(r);
             if (pos >= fl_next) {
                 flush(fl_done, fl_next);
                 fl_done = fl_next;

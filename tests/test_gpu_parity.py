@@ -196,3 +196,21 @@ def test_file_ingest_large_vs_oracle(tmp_path, device):
     exp_tot, _ = O.decompress_all(gz, oi, threads=8)
     assert tot == exp_tot == nrec
     assert pp.BatchedFASTQ(ix, str(p), True, device=device).Count() == nrec
+
+
+@pytest.mark.parametrize("nl_bytes", ["1099511627776", "1"])
+def test_census_capacity_extremes(nl_bytes, device, monkeypatch):
+    """The newline census fused into the inflate flush stores at most nl_cap positions per chunk;
+    chunks past it take the body-scan fallback (ppg_parse_emit).  Capacity 0 (every chunk with
+    newlines overflows) and capacity >= every byte must both give the golden record tables."""
+    monkeypatch.setenv("PPG_NL_BYTES", nl_bytes)
+    for name in CASES:
+        meta, gz = load_case(name)
+        ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+        n = ix.Count - 1
+        sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+        for k, c in enumerate(meta["chunks"]):
+            rec = sh.chunk_records(k)
+            assert len(rec) == c["records"], (name, k)
+            assert sha(np.ascontiguousarray(rec, "<u4").tobytes()) == c["rec_sha256"], (name, k)
+        assert sh.total_records == meta["total_records"]
