@@ -359,10 +359,30 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);       // length symbol: all ones
     const uint32_t tb = ((e >> 5) & 31) + (((d >> 5) & 31) & lm);
     const uint32_t nb = ((mlen - 1) & lm) + 1;                      // output bytes
-    const uint32_t sm = -(uint32_t)(((e & 15) == 0) | ((((d & 15) | ~lm)) == 0));   // special: all ones
+    // special: all ones (one v_min + v_cmp: no SALU mask arithmetic)
+    const uint32_t sm = min(e & 15u, (d & 15u) | ~lm) == 0u ? ~0u : 0u;
     const uint32_t field = ((dist - 1) & lm) | ((0x100u | (e >> 16)) & ~lm);
     const uint32_t tok = tb | (nb << 8) | (field << 17);
     return (tok & ~sm) | ((128u | (0x100u << 17)) & sm);
+}
+
+// The walk loop of the decoder (see Round): per token v_readlane (candidate X[5:0]),
+// v_writelane (at output offset (X >> 8)[5:0]), one s_add, and s_and's SCC as the loop test —
+// written out because the compiler adds an s_cmp_eq 0 after the s_and (one more SALU per token,
+// and SALU issue is what bounds this kernel).  The order is the compiler's own hazard-clean one.
+__device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
+    uint32_t t, tmp;
+    asm volatile(
+        "1:\n\t"
+        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc0 1b"
+        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
+        : [vt] "v"(vt)
+        : "m0", "scc");
 }
 
 // IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
@@ -614,19 +634,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 uint32_t X;
                 if (len - pos >= 64) {
                     X = off << 8;
+#ifdef PPG_WALK_C
                     do {
                         t = rdlane(vta, X);
                         vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
                         X += t;
                     } while ((X & STOP) == 0u);
+#else
+                    walk_asm(vta, vtin, X);
+#endif
                     if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
                         X -= 64;
                         half = 64;
+#ifdef PPG_WALK_C
                         do {
                             t = rdlane(vtb, X);
                             vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
                             X += t;
                         } while ((X & STOP) == 0u);
+#else
+                        walk_asm(vtb, vtin, X);
+#endif
                     }
                     off = (X >> 8) & 511u;
                 } else {
