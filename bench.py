@@ -61,10 +61,19 @@ def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
     recs, _ = O.decompress_all(gz, oi, threads=threads, first=0, last=sample)
     dt = time.perf_counter() - t
     out_bytes = int(ix_out[sample] - ix_out[0])
+    # SURVEY 8d variants: one thread, and the C#-shaped consumer that materialises every record
+    # into its own buffer as FastqRecord does (Parsing.cs:41-47, mode 1), on smaller prefixes
+    variants = {}
+    for name, th, mode, n in (("1 thread", 1, 0, min(sample, 256)),
+                              (f"{threads} threads, records materialised", threads, 1, min(sample, 2048))):
+        t1 = time.perf_counter()
+        r1, _ = O.decompress_all(gz, oi, threads=th, mode=mode, first=0, last=n)
+        d1 = time.perf_counter() - t1
+        variants[name] = {"records_per_s": r1 / d1, "cores": th, "chunks": n, "seconds": d1}
     return {"value": recs / dt, "unit": "records/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} of {nchunks} chunks ({recs:,} records, {out_bytes / 1e9:.2f} GB out) "
                       f"of the same file, {threads} threads, {dt:.2f} s",
-            "decompressed_MBps": out_bytes / dt / 1e6}
+            "decompressed_MBps": out_bytes / dt / 1e6, "variants": variants}
 
 
 def pmc_traffic(workload, launches_per_step):

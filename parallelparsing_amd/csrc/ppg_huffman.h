@@ -4,7 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define DB 8             // distance root table bits
+#ifndef PPG_DB
+#define PPG_DB 8
+#endif
+#define DB PPG_DB        // distance root table bits
 #define CB 7             // code-length-code table bits (complete: max code length is 7)
 
 // Root-table entries (the lane-parallel decoder's format).  Every field is placed so that one
