@@ -470,6 +470,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         }
     };
     uint32_t nblk = 0;
+#ifdef PPG_STATS
+    // debug build only (EXTRA=-DPPG_STATS): per-chunk round / token / path counts, printed for the
+    // first chunks (tools/ab_bench.sh-style runs; DESIGN.md quotes them)
+    uint32_t st_rounds = 0, st_tokens = 0, st_spec = 0, st_short = 0, st_far = 0, st_dep = 0, st_dbl = 0,
+             st_blit = 0, st_beob = 0, st_bmatch = 0;
+#endif
     // IX: record a block end (chunk-relative bit e); false = stop decoding
     auto block_end = [&](uint32_t e) -> bool {
         if (nblk >= J.blk_cap) { flags |= PPG_FLAG_BLK_FULL; return false; }
@@ -686,6 +692,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             // ---- one round: decode + walk, then one output byte per lane ----
             st_enter(r, S.stream, bp >> 10, lane);
             const Round R = decode(bp, cn, cw, pos);
+#ifdef PPG_STATS
+            st_rounds++;
+            st_tokens += (uint32_t)__popcll(__ballot(R.vtin != 0));
+            if (R.spec) st_spec++;
+            if (R.off < 64) st_short++;
+#endif
             const uint32_t tot = min(R.off, len - pos);   // output bytes of the round's tokens
             const uint32_t rout = min(tot, 64u);          // ... emitted this round
             const uint64_t mo = __ballot(R.vtin != 0);    // token start offsets (never 0 words)
@@ -701,6 +713,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
                 const uint64_t fm = __ballot(far);
+#ifdef PPG_STATS
+                if (fm) st_far++;
+#endif
                 if (fm) {
                     // older than the ring: the flushed output (this wave's own earlier stores), as
                     // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
@@ -718,7 +733,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
                     int32_t ptr = dep ? jj : lane;
+#ifdef PPG_STATS
+                    st_dep++;
+#endif
                     for (;;) {
+#ifdef PPG_STATS
+                        st_dbl++;
+#endif
                         const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
                         if (!__ballot(p2 != ptr)) break;
                         ptr = p2;
@@ -764,6 +785,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             rd_seek(r, S.stream, bp, lane);
             rd_refill(r, S.stream, lane);
             const int sym = canon_decode(r, clit, S.lit_sorted, lane);
+#ifdef PPG_STATS
+            if (sym < 256) st_blit++; else if (sym == 256) st_beob++; else st_bmatch++;
+#endif
             if (sym < 0 || sym >= 286) { status = ST_DATA_ERROR; break; }
             if (sym < 256) {
                 if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)sym;
@@ -811,6 +835,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         if (canon_decode(r, clit, S.lit_sorted, lane) == 256) end_bit = rd_pos(r);
         else flags |= PPG_FLAG_NO_EOB;
     }
+#ifdef PPG_STATS
+    if (!IX && lane == 0 && k < 4)
+        printf("PPG_STATS chunk %d: bytes %u rounds %u tokens %u spec %u short %u far %u dep %u dbl %u "
+               "bitserial lit %u eob %u match %u\n", k, pos, st_rounds, st_tokens, st_spec, st_short, st_far, st_dep,
+               st_dbl, st_blit, st_beob, st_bmatch);
+#endif
     if (lane == 0) {
         res[k].produced = pos;
         res[k].end_bit = w0abs * 32 + end_bit;
