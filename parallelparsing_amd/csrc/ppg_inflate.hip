@@ -296,6 +296,17 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, con
     return dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
 }
 
+// One dword per lane from a uniform base + 32-bit lane offset, as global_load_dword's saddr form,
+// and the wait for it.  Written out because the compiler turns the emit's far-byte load into
+// exec-mask juggling (~9 SALU per round) or a 64-bit per-lane address; the caller waits with
+// far_wait before using the value (the "+v" operand orders the use after the wait).
+__device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
+    return v;
+}
+__device__ __forceinline__ void far_wait(uint32_t &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)::"memory"); }
+
 // One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
 template <int RB, bool IX>
 __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uint32_t oa, const uint8_t *dict,
@@ -723,10 +734,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     const int32_t p = (int32_t)pos + jj;
                     const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
                     const bool fo = far && p >= 0;
-                    const uint32_t w = *(const uint32_t *)(ob + (fo ? (q & ~3u) : 0u));
-                    if (fo) val = (w >> (8 * (q & 3))) & 255u;
-                    if (__ballot(far && p < 0)) {
-                        if (far && p < 0) val = dict[32768u + (uint32_t)p];   // p >= -32768
+                    uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
+                    far_wait(w);
+                    val = fo ? (w >> (8 * (q & 3))) & 255u : val;
+                    const bool fd = far && p < 0;
+                    const uint64_t dm = __ballot(fd);
+                    if (dm) {   // rare: the chunk's first 32 KiB
+                        const uint32_t db = dict[fd ? 32768u + (uint32_t)p : 0u];   // p >= -32768
+                        val = fd ? db : val;
                     }
                 }
                 const bool dep = jj >= 0;                             // produced in this round
