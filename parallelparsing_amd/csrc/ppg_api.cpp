@@ -41,7 +41,8 @@ hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgIn
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n);
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
-                                 PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs, int n);
+                                 PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs,
+                                 uint64_t cap, int n);
 hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   const PpgParseInfo *info, const uint64_t *base, const uint32_t *recs, int64_t *keys,
@@ -383,6 +384,8 @@ struct ppg_shard {
     int64_t total_records = 0;
     float t_inflate = 0, t_parse = 0, t_total = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t stream = nullptr;   // null: the ctx stream (ppg_file_decompress_all gives each piece shard its own)
+    uint64_t *h_tot = nullptr;      // pinned: a batch's record total, read back without a stream sync
     int ran = 0;
 };
 
@@ -392,6 +395,7 @@ void ppg_shard_free(ppg_shard *sh) {
     if (!sh) return;
     (void)hipSetDevice(sh->ctx->device);
     for (auto &e : sh->ev) if (e) (void)hipEventDestroy(e);
+    if (sh->h_tot) (void)hipHostFree(sh->h_tot);
     delete sh;
 }
 
@@ -507,6 +511,7 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
     HIPCHK(sh->nls.alloc((size_t)nl_need + 64));
     if (!sh->ev[0])
         for (auto &e : sh->ev) HIPCHK(hipEventCreate(&e));
+    if (!sh->h_tot) HIPCHK(hipHostMalloc((void **)&sh->h_tot, 8, hipHostMallocDefault));
     HIPCHK(hipStreamSynchronize(s));   // the host staging vectors above die here
     return PPG_OK;
 }
@@ -534,55 +539,103 @@ int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n
     return PPG_OK;
 }
 
-int ppg_shard_run(ppg_shard *sh) {
-    if (!sh) return PPG_ARG_ERROR;
-    HIPCHK(hipSetDevice(sh->ctx->device));
-    hipStream_t s = sh->ctx->stream;
+}  // extern "C"
+
+static hipStream_t shard_stream(const ppg_shard *sh) { return sh->stream ? sh->stream : sh->ctx->stream; }
+
+static void shard_reset(ppg_shard *sh) {
     sh->t_inflate = sh->t_parse = sh->t_total = 0;
     sh->h_base.assign((size_t)sh->n, 0);
     sh->total_records = 0;
-    float total_ms = 0;
-    for (auto [b0, b1] : sh->batches) {
-        const int nb = b1 - b0;
-        HIPCHK(hipEventRecord(sh->ev[0], s));
-        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords, sh->jobs.p + b0,
-                                  sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
-        HIPCHK(hipEventRecord(sh->ev[1], s));
-        HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
-                                      sh->info.p + b0, sh->base.p + b0, sh->total.p, nb));
-        uint64_t tot = 0;
-        HIPCHK(hipMemcpyAsync(&tot, sh->total.p, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if ((size_t)(4 * tot) > sh->recs.n) HIPCHK(sh->recs.alloc((size_t)(4 * tot + 4096)));
+    sh->ran = 0;
+}
+
+// Enqueue one batch [b0, b1) on the shard's stream, with no host synchronisation: inflate (+ the
+// fused newline census), per-chunk counts and their scan, the record total into pinned host
+// memory, then the descriptors, whose writes stop at the descriptor buffer's size.
+static int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
+    hipStream_t s = shard_stream(sh);
+    const int nb = b1 - b0;
+    HIPCHK(hipEventRecord(sh->ev[0], s));
+    HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
+                              sh->jobs.p + b0, sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
+    HIPCHK(hipEventRecord(sh->ev[1], s));
+    HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
+                                  sh->info.p + b0, sh->base.p + b0, sh->total.p, nb));
+    HIPCHK(hipMemcpyAsync(sh->h_tot, sh->total.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(sh->ev[2], s));
+    HIPCHK(ppg_launch_parse_emit(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
+                                 sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p, (uint64_t)sh->recs.n, nb));
+    HIPCHK(hipEventRecord(sh->ev[3], s));
+    return PPG_OK;
+}
+
+// Wait for a launched batch.  If its records did not fit the descriptor buffer (more than one
+// record per 256 output bytes), grow the buffer and write the descriptors again.
+static int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms) {
+    hipStream_t s = shard_stream(sh);
+    const int nb = b1 - b0;
+    HIPCHK(hipEventSynchronize(sh->ev[3]));
+    const uint64_t tot = *sh->h_tot;
+    float a = 0, b = 0, c = 0;
+    HIPCHK(hipEventElapsedTime(&a, sh->ev[0], sh->ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, sh->ev[1], sh->ev[2]));   // counts + scan
+    HIPCHK(hipEventElapsedTime(&c, sh->ev[2], sh->ev[3]));   // descriptors
+    if ((size_t)(4 * tot) > sh->recs.n) {
+        HIPCHK(sh->recs.alloc((size_t)(4 * tot + 4096)));
         HIPCHK(hipEventRecord(sh->ev[2], s));
         HIPCHK(ppg_launch_parse_emit(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
-                                     sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p, nb));
+                                     sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p, (uint64_t)sh->recs.n,
+                                     nb));
         HIPCHK(hipEventRecord(sh->ev[3], s));
         HIPCHK(hipEventSynchronize(sh->ev[3]));
-        float a = 0, b = 0, c = 0;
-        HIPCHK(hipEventElapsedTime(&a, sh->ev[0], sh->ev[1]));
-        HIPCHK(hipEventElapsedTime(&b, sh->ev[1], sh->ev[2]));   // count + scan (+ host read of the total)
-        HIPCHK(hipEventElapsedTime(&c, sh->ev[2], sh->ev[3]));
-        sh->t_inflate += a;
-        sh->t_parse += b + c;
-        total_ms += a + b + c;
-        // batch-local bases -> shard-global
-        std::vector<uint64_t> hb((size_t)nb);
-        HIPCHK(hipMemcpy(hb.data(), sh->base.p + b0, 8 * (size_t)nb, hipMemcpyDeviceToHost));
-        for (int i = 0; i < nb; i++) sh->h_base[(size_t)(b0 + i)] = (int64_t)hb[(size_t)i] + sh->total_records;
-        sh->total_records += (int64_t)tot;
+        float c2 = 0;
+        HIPCHK(hipEventElapsedTime(&c2, sh->ev[2], sh->ev[3]));
+        c += c2;
     }
+    sh->t_inflate += a;
+    sh->t_parse += b + c;
+    total_ms += a + b + c;
+    // batch-local bases -> shard-global
+    std::vector<uint64_t> hb((size_t)nb);
+    HIPCHK(hipMemcpyAsync(hb.data(), sh->base.p + b0, 8 * (size_t)nb, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < nb; i++) sh->h_base[(size_t)(b0 + i)] = (int64_t)hb[(size_t)i] + sh->total_records;
+    sh->total_records += (int64_t)tot;
+    return PPG_OK;
+}
+
+static int shard_finish(ppg_shard *sh, float total_ms) {
+    hipStream_t s = shard_stream(sh);
     sh->t_total = total_ms;
     sh->h_res.resize((size_t)sh->n);
     sh->h_info.resize((size_t)sh->n);
     if (sh->n) {
-        HIPCHK(hipMemcpy(sh->h_res.data(), sh->res.p, sizeof(PpgInflateResult) * (size_t)sh->n, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(sh->h_info.data(), sh->info.p, sizeof(PpgParseInfo) * (size_t)sh->n, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(sh->h_res.data(), sh->res.p, sizeof(PpgInflateResult) * (size_t)sh->n,
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(sh->h_info.data(), sh->info.p, sizeof(PpgParseInfo) * (size_t)sh->n,
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
     }
     sh->ran = 1;
     for (int32_t i = 0; i < sh->n; i++)
         if (sh->h_res[(size_t)i].status != 0) return sh->h_res[(size_t)i].status;
     return PPG_OK;
+}
+
+extern "C" {
+
+int ppg_shard_run(ppg_shard *sh) {
+    if (!sh) return PPG_ARG_ERROR;
+    HIPCHK(hipSetDevice(sh->ctx->device));
+    shard_reset(sh);
+    float total_ms = 0;
+    for (auto [b0, b1] : sh->batches) {
+        int rc = batch_launch(sh, b0, b1);
+        if (rc == PPG_OK) rc = batch_collect(sh, b0, b1, total_ms);
+        if (rc != PPG_OK) return rc;
+    }
+    return shard_finish(sh, total_ms);
 }
 
 int ppg_shard_results(ppg_shard *sh, int64_t *records, int64_t *produced, int32_t *status, int32_t *flags,
@@ -712,24 +765,27 @@ bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads)
 
 }  // namespace
 
-constexpr int kSlots = 4;                        // pinned staging slots
+constexpr int kSlots = 4;     // pinned staging slots
+constexpr int kPieces = 3;   // device piece slots: one finishing, one decoding, one filling
 constexpr int64_t kSlotBytes = (int64_t)128 << 20;
 
 struct IngestState {
     PinnedBuf slot[kSlots];       // pinned host staging, streamed through round-robin
     hipEvent_t slot_ev[kSlots] = {};
-    DevBuf<uint8_t> db[2];        // device copies of two pieces (one decoding, one filling)
+    DevBuf<uint8_t> db[kPieces];  // device copies of pieces
     hipStream_t cs = nullptr;     // copy stream
-    ppg_shard *sh[2] = {nullptr, nullptr};
+    hipStream_t ks[kPieces] = {};   // decode streams, one per piece slot
+    ppg_shard *sh[kPieces] = {};
 };
 
 static void ingest_free(IngestState *st) {
     if (!st) return;
     for (int i = 0; i < kSlots; i++)
         if (st->slot_ev[i]) (void)hipEventDestroy(st->slot_ev[i]);
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < kPieces; i++)
         if (st->sh[i]) ppg_shard_free(st->sh[i]);
     if (st->cs) (void)hipStreamDestroy(st->cs);
+    for (auto &k : st->ks) if (k) (void)hipStreamDestroy(k);
     delete st;
 }
 
@@ -751,7 +807,9 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
     if (fd < 0) return PPG_IO_ERROR;
     struct FdClose { int fd; ~FdClose() { close(fd); } } fdc{fd};
 
-    // pieces: consecutive chunks of about piece_bytes compressed bytes (at least one chunk)
+    // pieces: consecutive chunks of about piece_bytes compressed bytes (at least one chunk).
+    // (Ramping the first / last pieces down measured slower: one chunk alone takes ~100 ms, so
+    // small pieces neither start nor drain the GPU faster.)
     std::vector<std::pair<int32_t, int32_t>> pieces;
     int64_t maxlen = 0;
     for (int32_t a = 0; a < n;) {
@@ -775,13 +833,15 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             HIPCHK(hipEventCreateWithFlags(&st->slot_ev[i], hipEventDisableTiming));
             HIPCHK(st->slot[i].alloc((size_t)kSlotBytes));
         }
-        for (int i = 0; i < 2; i++) {
+        for (int i = 0; i < kPieces; i++) {
             st->sh[i] = new ppg_shard;
             st->sh[i]->ctx = ctx;
+            HIPCHK(hipStreamCreateWithFlags(&st->ks[i], hipStreamNonBlocking));
+            st->sh[i]->stream = st->ks[i];
         }
     }
     IngestState &S = *ctx->ingest;
-    for (int i = 0; i < 2; i++) HIPCHK(S.db[i].alloc((size_t)maxlen + 64));
+    for (int i = 0; i < kPieces; i++) HIPCHK(S.db[i].alloc((size_t)maxlen + 64));
     if (verbose) fprintf(stderr, "[ingest] %zu pieces, max %.1f MB, setup %.1f ms\n", pieces.size(), maxlen / 1e6, now_ms());
 
     // Producer thread: piece k -> device buffer k&1 (pread into pinned slots, H2D on the copy
@@ -800,13 +860,13 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
         for (size_t k = 0; k < np && rcp == PPG_OK; k++) {
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop || k < done + 2; });
+                cv.wait(lk, [&] { return stop || k < done + kPieces; });
                 if (stop) return;
             }
             const double t1 = now_ms();
             int64_t off, len;
             range(k, off, len);
-            uint8_t *dst = S.db[k & 1].p;
+            uint8_t *dst = S.db[k % kPieces].p;
             for (int64_t r = 0; r < len && rcp == PPG_OK; r += kSlotBytes, slot = (slot + 1) % kSlots) {
                 const int64_t m = std::min(kSlotBytes, len - r);
                 if (hipEventSynchronize(S.slot_ev[slot]) != hipSuccess) { rcp = PPG_DEVICE_ERROR; break; }
@@ -818,7 +878,7 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             const double t2 = now_ms();
             if (rcp == PPG_OK && hipMemsetAsync(dst + len, 0, 64, S.cs) != hipSuccess) rcp = PPG_DEVICE_ERROR;
             if (rcp == PPG_OK)
-                rcp = shard_prepare(S.sh[k & 1], ix, first + pieces[k].first, pieces[k].second - pieces[k].first, dst,
+                rcp = shard_prepare(S.sh[k % kPieces], ix, first + pieces[k].first, pieces[k].second - pieces[k].first, dst,
                                     len, 0, S.cs);
             if (verbose)
                 fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms, prepare %.1f ms\n", k,
@@ -835,32 +895,46 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
         ~Joiner() { { std::lock_guard<std::mutex> lk(m); stop = true; } c.notify_all(); if (t.joinable()) t.join(); }
     } joiner{prod, mu, cv, stop};
 
+    // Consumer: piece k is launched on its own stream as soon as it is ready, and only then is
+    // piece k-1 collected, so piece k's waves fill the CUs that piece k-1's last waves leave idle
+    // (a piece is ~1.1 generations of resident waves: its tail would otherwise idle the GPU).
     int64_t total = 0;
     int rc = PPG_OK;
+    auto collect = [&](size_t k) -> int {
+        ppg_shard *sh = S.sh[k % kPieces];
+        float ms = 0;
+        int r = batch_collect(sh, 0, sh->n, ms);
+        if (r == PPG_OK) r = shard_finish(sh, ms);
+        const int32_t a = pieces[k].first, b = pieces[k].second;
+        if (verbose)
+            fprintf(stderr, "[ingest] piece %zu: %d chunks collected at %.1f ms (kernels %.1f)\n", k, b - a, now_ms(),
+                    sh->t_total);
+        if (sh->ran) {
+            for (int32_t i = 0; i < b - a; i++) {
+                const int64_t r2 = (int64_t)sh->h_info[(size_t)i].records;
+                if (records) records[a + i] = r2;
+                total += r2;
+            }
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        done = k + 1;
+        cv.notify_all();
+        return r;
+    };
     for (size_t k = 0; k < np; k++) {
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return ready > k || prod_rc != PPG_OK; });
             if (ready <= k) { rc = prod_rc; break; }
         }
-        const int32_t a = pieces[k].first, b = pieces[k].second;
-        const double tr = now_ms();
-        rc = ppg_shard_run(S.sh[k & 1]);
-        if (verbose)
-            fprintf(stderr, "[ingest] piece %zu: %d chunks, run at %.1f ms in %.1f ms (kernels %.1f)\n", k, b - a, tr,
-                    now_ms() - tr, S.sh[k & 1]->t_total);
-        if (rc == PPG_OK || S.sh[k & 1]->ran) {
-            for (int32_t i = 0; i < b - a; i++) {
-                const int64_t r = (int64_t)S.sh[k & 1]->h_info[(size_t)i].records;
-                if (records) records[a + i] = r;
-                total += r;
-            }
-        }
-        std::lock_guard<std::mutex> lk(mu);
-        done = k + 1;
-        cv.notify_all();
+        ppg_shard *sh = S.sh[k % kPieces];
+        shard_reset(sh);
+        rc = sh->batches.size() == 1 ? batch_launch(sh, 0, sh->n) : PPG_ARG_ERROR;
+        if (verbose) fprintf(stderr, "[ingest] piece %zu: launched at %.1f ms\n", k, now_ms());
         if (rc != PPG_OK) break;
+        if (k > 0 && (rc = collect(k - 1)) != PPG_OK) break;
     }
+    if (rc == PPG_OK && np > 0) rc = collect(np - 1);
     hipStream_t cs = S.cs;
     HIPCHK(hipStreamSynchronize(cs));
     HIPCHK(hipStreamSynchronize(ctx->stream));

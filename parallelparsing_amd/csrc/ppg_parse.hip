@@ -50,7 +50,7 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_finish(const PpgInfl
 extern "C" __global__ __launch_bounds__(64) void ppg_parse_serial(
     const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
     const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, PpgParseInfo *__restrict__ info,
-    const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks, int mode) {
+    const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks, int mode, uint64_t cap) {
     const int k = blockIdx.x;
     if (k >= nchunks || threadIdx.x != 0) return;
     if (!info[k].serial || ires[k].status != 0) return;
@@ -78,7 +78,7 @@ extern "C" __global__ __launch_bounds__(64) void ppg_parse_serial(
             i++;
         }
         if (!ok) break;
-        if (dst) {
+        if (dst && 4 * (base[k] + n) + 4 <= cap) {   // cap: the descriptor buffer's u32 entries
             dst[4 * n + 0] = (uint32_t)nn[0];
             dst[4 * n + 1] = (uint32_t)nn[1];
             dst[4 * n + 2] = (uint32_t)nn[2];
@@ -117,7 +117,7 @@ extern "C" __global__ __launch_bounds__(1024) void ppg_scan_counts(const PpgPars
 extern "C" __global__ __launch_bounds__(256) void ppg_parse_emit(
     const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
     const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, const PpgParseInfo *__restrict__ info,
-    const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks) {
+    const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks, uint64_t cap) {
     const int k = blockIdx.x;
     if (k >= nchunks) return;
     if (!info[k].emit || info[k].serial || ires[k].status != 0) return;
@@ -125,6 +125,7 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_emit(
     __shared__ uint32_t wsum[4];
     const uint64_t nrec = info[k].records;
     if (nrec == 0) return;
+    if (4 * (base[k] + nrec) > cap) return;   // the host grows the buffer and runs this again
     const uint64_t limit = 4 * nrec;
     uint32_t *dst = recs + 4 * base[k];
     const uint8_t *off = offs + oref[k].start;
@@ -186,11 +187,12 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_emit(
 extern "C" __global__ __launch_bounds__(256) void ppg_parse_place(
     const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires, const uint8_t *__restrict__ offs,
     const PpgOffsetRef *__restrict__ oref, const PpgParseInfo *__restrict__ info, const uint64_t *__restrict__ base,
-    const uint32_t *__restrict__ nls, uint32_t *__restrict__ recs, int nchunks) {
+    const uint32_t *__restrict__ nls, uint32_t *__restrict__ recs, int nchunks, uint64_t cap) {
     const int k = blockIdx.x;
     if (k >= nchunks) return;
     const PpgParseInfo f = info[k];
     if (f.serial || f.emit || ires[k].status != 0 || f.records == 0) return;
+    if (4 * (base[k] + f.records) > cap) return;   // the host grows the buffer and runs this again
     const uint64_t limit = 4 * f.records;
     uint32_t *dst = recs + 4 * base[k];
     const uint32_t onl = oref[k].nl & ~PPG_OFF_SERIAL;
@@ -258,7 +260,7 @@ hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgIn
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(ppg_parse_finish, dim3((n + 255) / 256), dim3(256), 0, s, ires, oref, info, n);
     hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info,
-                       (const uint64_t *)nullptr, (uint32_t *)nullptr, n, 0);
+                       (const uint64_t *)nullptr, (uint32_t *)nullptr, n, 0, (uint64_t)0);
     hipLaunchKernelGGL(ppg_scan_counts, dim3(1), dim3(1024), 0, s, info, base, total, n);
     return hipGetLastError();
 }
@@ -266,11 +268,12 @@ hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgIn
 // descriptors: census copy (most chunks), body scan (census overflow), serial machine (R-P3 fails)
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
-                                 PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs, int n) {
+                                 PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs,
+                                 uint64_t cap, int n) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_parse_place, dim3(n), dim3(256), 0, s, jobs, ires, offs, oref, info, base, nls, recs, n);
-    hipLaunchKernelGGL(ppg_parse_emit, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, n);
-    hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, 1);
+    hipLaunchKernelGGL(ppg_parse_place, dim3(n), dim3(256), 0, s, jobs, ires, offs, oref, info, base, nls, recs, n, cap);
+    hipLaunchKernelGGL(ppg_parse_emit, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, cap);
+    hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, 1, cap);
     return hipGetLastError();
 }
 
