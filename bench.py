@@ -174,6 +174,77 @@ def create_index_run(tf, args, dev):
                               "projected_seconds_full_member": text / 1e9 / cpu_gbs}}
 
 
+def paired_run(args, dev):
+    """BASELINE configs[4]-shaped paired-end run on one GPU: two tiled members (R1 / R2 of a read
+    pair: equal spot numbers, different SRR ids and bases), chunk = 50,000, both decoded and
+    resident, every record's spot key extracted on the GPU, Q1 duplicates dropped and the pair
+    invariant checked on the device (paired.PairedFASTQ's path).  Size per file: --paired-repeats
+    segments (default ~12.5 GB gz each: both decoded outputs must stay resident for pairing)."""
+    import torch
+    import parallelparsing_amd as pp
+    from parallelparsing_amd import paired
+    from parallelparsing_amd.tiled import TiledFile
+    t = time.time()
+    tfs = [TiledFile(args.seg_records, args.paired_repeats, 50_000, seed=m - 1, mate=m, threads=args.host_threads)
+           for m in (1, 2)]
+    log(f"[bench] paired input: 2 x {tfs[0].records * tfs[0].repeats:,} records, "
+        f"{tfs[0].file_len / 1e9:.2f} + {tfs[1].file_len / 1e9:.2f} GB gz, built in {time.time() - t:.1f}s")
+    # one ctx (= one HIP stream) per file, so the two DecompressAll passes run concurrently: at
+    # chunk = 50,000 one file has only ~2.7k chunks, a third of the GPU's 8k wave slots
+    ctxs = [pp.Device(dev.index), pp.Device(dev.index)]
+    shards, bufs = [], []
+    for tf, ctx in zip(tfs, ctxs):
+        lo, hi = int(tf.p_input[0]) - 1, int(tf.p_input[-1])
+        comp = torch.empty(hi - lo + 256, dtype=torch.uint8, device=dev)
+        comp[hi - lo:].zero_()
+        tf.fill_device(comp, lo, hi)
+        bufs.append(comp)
+        out_cap = int(tf.p_output[-1] - tf.p_output[0]) + (1 << 20)
+        shards.append(pp.Shard(tf.index(0, tf.npoints), comp.data_ptr(), first=0, n=tf.npoints - 1, device=ctx,
+                               comp_on_device=True, comp_len=hi - lo, out_capacity=out_cap))
+    torch.cuda.synchronize()
+
+    import threading
+
+    def step():
+        th = [threading.Thread(target=sh.run) for sh in shards]   # ctypes drops the GIL
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        keys = [paired.dedup(paired.shard_keys(sh))[0] for sh in shards]
+        return paired.check_pairs(keys[0], keys[1])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        npairs = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    assert npairs == tfs[0].records * tfs[0].repeats, (npairs, tfs[0].records * tfs[0].repeats)
+    text = sum(int(tf.p_output[-1] - tf.p_output[0]) for tf in tfs)
+    return {
+        "metric": "paired-end record pairs/sec (R1+R2 DecompressAll + on-GPU pair check), 1 MI355X",
+        "value": npairs * args.steps / elapsed,
+        "unit": "pairs/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (Generator-shape 150 bp read pairs, tiled single gzip members, zlib level 6)",
+        "config": {"workload": f"configs[4]-shaped: 2 x {tfs[0].file_len / 1e9:.1f} GB .fastq.gz on one GPU, "
+                               f"chunk=50000, pair chunks of 50,000 records",
+                   "pairs": npairs, "gz_bytes": [tf.file_len for tf in tfs], "decompressed_bytes": text},
+        "decompressed_MBps": text * args.steps / elapsed / 1e6,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +259,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--create-index", action="store_true",
                     help="also time the GPU CreateIndex over the whole member (reported under 'create_index')")
+    ap.add_argument("--paired", action="store_true",
+                    help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
+    ap.add_argument("--paired-repeats", type=int, default=51)   # ~12.5 GB gz per file
     ap.add_argument("--ingest", action="store_true",
                     help="also time DecompressAll straight from the .gz file on disk (host ingest, PCIe-inclusive; "
                          "reported under 'ingest', never as value)")
@@ -208,6 +282,11 @@ def main():
 
     import parallelparsing_amd as pp
     from parallelparsing_amd.dist import partition_chunks, gather_counts
+
+    if args.paired:
+        assert world == 1, "--paired runs on one GPU (the multi-GPU pair exchange: paired.distributed_pair_check)"
+        print(json.dumps(paired_run(args, dev)), flush=True)
+        return
 
     tf = build_input(args)
     ix_out, ix_in = tf.p_output, tf.p_input
