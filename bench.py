@@ -38,7 +38,10 @@ def build_input(args):
     t = time.time()
     if args.workload == "50gb":
         # weak scaling: the member holds `repeats` segments per rank (~50 GB of gzip per GPU)
-        tf = TiledFile(args.seg_records, args.repeats * args.world, args.chunk, threads=args.host_threads)
+        # weak (default): ~50 GB of gzip per GPU; strong: one ~50 GB member split over the GPUs
+        # (BASELINE configs[3] literally)
+        reps = args.repeats * (args.world if args.scaling == "weak" else 1)
+        tf = TiledFile(args.seg_records, reps, args.chunk, threads=args.host_threads)
     else:  # 1m: configs[1], one non-repeated 1 M-read member
         tf = TiledFile(1_000_000, 1, args.chunk, threads=args.host_threads)
     log(f"[bench] input: {tf.records * tf.repeats:,} records, {tf.text_len * tf.repeats / 1e9:.1f} GB text, "
@@ -254,6 +257,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=10000)
     ap.add_argument("--seg-records", type=int, default=2_621_440)   # ~1 GB of text per segment
     ap.add_argument("--repeats", type=int, default=203)             # per GPU: ~50 GB gz, ~532 M records
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: ~50 GB of gzip per GPU (default); strong: one ~50 GB member over N GPUs")
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -358,8 +363,9 @@ def main():
     launches = shard.batches * args.steps
     mean_launch_s = infl_ms / 1e3 / launches
     achieved = alg_local / shard.batches / mean_launch_s / 1e9
-    workload = ("configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000" if args.workload == "50gb"
-                else "configs[1]: 1 M-read .fastq.gz, chunk=10000")
+    workload = ("configs[1]: 1 M-read .fastq.gz, chunk=10000" if args.workload != "50gb"
+                else "configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000" if args.scaling == "weak" or world == 1
+                else f"configs[3]: ~50 GB .fastq.gz sharded across {world} GPUs, chunk=10000")
     line = {
         "metric": "FASTQ records/sec + decompressed MB/s, 50 GB .fastq.gz, 1/2/4/8 MI355X",
         "value": rec_s,
@@ -369,7 +375,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)",
