@@ -297,15 +297,15 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, con
 }
 
 // One dword per lane from a uniform base + 32-bit lane offset, as global_load_dword's saddr form,
-// and the wait for it.  Written out because the compiler turns the emit's far-byte load into
-// exec-mask juggling (~9 SALU per round) or a 64-bit per-lane address; the caller waits with
-// far_wait before using the value (the "+v" operand orders the use after the wait).
+// waited for in the same asm statement (so no copy of the register can be read while the load is
+// in flight).  Written out because the compiler turns the emit's far-byte load into exec-mask
+// juggling (~9 SALU per round) or a 64-bit per-lane address.  The wait also covers the stream's
+// LDS-DMA issued before it, as any vmcnt wait here did.
 __device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) {
     uint32_t v;
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
+    asm volatile("global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
     return v;
 }
-__device__ __forceinline__ void far_wait(uint32_t &v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)::"memory"); }
 
 // One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
 template <int RB, bool IX>
@@ -734,8 +734,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     const int32_t p = (int32_t)pos + jj;
                     const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
                     const bool fo = far && p >= 0;
-                    uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
-                    far_wait(w);
+                    const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
                     val = fo ? (w >> (8 * (q & 3))) & 255u : val;
                     const bool fd = far && p < 0;
                     const uint64_t dm = __ballot(fd);
