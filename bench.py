@@ -166,7 +166,7 @@ def create_index_run(tf, args, dev):
     cpu_gbs = one.text_len / csec / 1e9
     return {"seconds": sec, "first_run_s": runs[0], "points": ix.Count, "gz_GBps": tf.file_len / sec / 1e9,
             "decompressed_GBps": text / sec / 1e9,
-            "phases_ms": {k: round(st[k], 2) for k in ("finder_ms", "pass1_ms", "chain_ms", "resolve_ms", "pass2_ms",
+            "phases_ms": {k: round(st[k], 2) for k in ("finder_ms", "pass1_ms", "chain_ms", "resolve_ms", "pass2_ms", "pass2_alloc_ms",
                                                        "census_ms")},
             "pieces": int(st["pieces"]), "real_pieces": int(st["real_pieces"]), "redo1": int(st["redo1"]),
             "pass2_batches": int(st["batches"]),

@@ -266,7 +266,7 @@ class Core:
 
     GPU_INDEX_STATS = ("finder_ms", "pass1_ms", "chain_ms", "pass2_ms", "census_ms", "total_ms", "pieces",
                        "real_pieces", "redo1", "resolve_ms", "batches", "blocks", "points", "output_bytes",
-                       "upload_ms")
+                       "upload_ms", "pass2_alloc_ms")
 
     @staticmethod
     def gpu_index_stats(device=None):

@@ -381,6 +381,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     DevBuf<uint8_t> out;
     HIPCHK(out.alloc((size_t)cap + 64));
     HIPCHK(hipMemsetAsync(out.p + cap, 0, 64, s));
+    stat[15] = ms_since(t);   // the pass-2 output buffer's allocation
     DevBuf<PpgInflateJob> jobs2;
     DevBuf<PpgInflateResult> res2;
     DevBuf<uint8_t> tmp;                // pass-2 tails of a batch (checked against W)
