@@ -124,6 +124,19 @@ void ppg_shard_free(ppg_shard *sh);
  * 63-74, for all chunks).  Returns 0, or the first chunk error (ZResult code).  Blocking. */
 int ppg_shard_run(ppg_shard *sh);
 
+/* Parallelism inside chunks (no reference counterpart: the reference decodes a chunk on one
+ * thread, Core.cs:133-192; SURVEY §8f #1 "a denser side-index for sub-chunk parallelism").
+ * nsub side points, sorted by output, each a deflate block start strictly inside one of the
+ * shard's chunks: absolute file bit position (8*Input - Bits in Point terms), absolute output
+ * offset, and the 32 KiB of output before it (host array, nsub * 32768 bytes).  Later runs decode
+ * each chunk as one wave per piece between its Point, its side points and the next Point, and
+ * fold the pieces back into the chunk (ppg_split_merge): results, records and bytes are
+ * identical to the unsplit run.  A side point that is not where the previous piece's blocks end
+ * fails the chunk with PPG_DATA_ERROR.  Needs a one-batch shard (else PPG_UNSUPPORTED);
+ * nsub = 0 restores one wave per chunk. */
+int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
+                        const uint8_t *windows);
+
 /* Per-chunk results of the last run (host arrays of length n; any may be NULL). */
 int ppg_shard_results(ppg_shard *sh, int64_t *records, int64_t *produced, int32_t *status, int32_t *flags,
                       int64_t *end_bit);

@@ -337,6 +337,21 @@ class Shard:
     def batches(self):
         return lib.ppg_shard_batches(self._h)
 
+    def set_split(self, bits, outputs, windows):
+        """Decode chunks as several waves each, split at side points (deflate block starts inside
+        the chunks: absolute bit, absolute output, 32 KiB window each; ppg_shard_set_split).
+        Empty arrays restore one wave per chunk.  Results are identical either way."""
+        bits = np.ascontiguousarray(bits, np.int64)
+        outputs = np.ascontiguousarray(outputs, np.int64)
+        windows = np.ascontiguousarray(windows, np.uint8)
+        n = int(bits.size)
+        if outputs.size != n or windows.size != n * 32768:
+            raise ValueError("set_split: bits, outputs and windows (n * 32768 bytes) must agree")
+        self._split = (bits, outputs, windows)
+        check(lib.ppg_shard_set_split(self._h, n, _ptr(bits) if n else None, _ptr(outputs) if n else None,
+                                      _ptr(windows) if n else None), "set_split")
+        return self
+
     def results(self):
         n = self.n
         rec, prod, end = (np.zeros(n, np.int64) for _ in range(3))

@@ -88,6 +88,7 @@ _SIGS = {
     "ppg_shard_results": (C.c_int, [vp, vp, vp, vp, vp, vp]),
     "ppg_shard_total_records": (i64, [vp]),
     "ppg_shard_batches": (i32, [vp]),
+    "ppg_shard_set_split": (C.c_int, [vp, i32, vp, vp, vp]),
     "ppg_shard_copy_chunk": (C.c_int, [vp, i32, vp, i64, P(i64)]),
     "ppg_shard_copy_records": (C.c_int, [vp, i32, vp, i64, P(i64)]),
     "ppg_shard_record_base": (C.c_int, [vp, vp]),

@@ -39,6 +39,9 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n);
+hipError_t ppg_launch_split_merge(hipStream_t s, const PpgInflateJob *sjobs, const PpgInflateResult *sres,
+                                  const uint32_t *sidx, const uint32_t *snls, const PpgInflateJob *jobs,
+                                  PpgInflateResult *res, uint32_t *nls, int n);
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                  PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs,
@@ -387,6 +390,16 @@ struct ppg_shard {
     hipStream_t stream = nullptr;   // null: the ctx stream (ppg_file_decompress_all gives each piece shard its own)
     uint64_t *h_tot = nullptr;      // pinned: a batch's record total, read back without a stream sync
     int ran = 0;
+    // split chunks (ppg_shard_set_split): the inflate launch runs sub-jobs, ppg_split_merge folds
+    // them back into per-chunk results and census regions
+    int32_t nsub = 0;                            // side points in use (0: one wave per chunk)
+    int64_t base_byte = 0;                       // file byte of comp[0]
+    std::vector<int64_t> h_pout;                 // Output of points first .. first + n
+    std::vector<PpgInflateJob> h_sjobs;
+    DevBuf<PpgInflateJob> sjobs;
+    DevBuf<PpgInflateResult> sres;
+    DevBuf<uint32_t> sidx;                      // chunk k = sub-jobs [sidx[k], sidx[k+1])
+    DevBuf<uint32_t> snls;                      // the sub-jobs' own census regions
 };
 
 extern "C" {
@@ -414,6 +427,10 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
     if (((uintptr_t)comp & 3) != 0) return PPG_ARG_ERROR;
     sh->first = first;
     sh->n = n;
+    sh->base_byte = base_byte;
+    sh->h_pout.resize((size_t)n + 1);
+    for (int32_t i = 0; i <= n; i++) sh->h_pout[(size_t)i] = P[(size_t)first + i].output;
+    sh->nsub = 0;
     sh->comp = comp;
     sh->comp_len = comp_len;
     sh->nwords = (uint64_t)(comp_len + 3) / 4;
@@ -557,8 +574,16 @@ static int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     hipStream_t s = shard_stream(sh);
     const int nb = b1 - b0;
     HIPCHK(hipEventRecord(sh->ev[0], s));
-    HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
-                              sh->jobs.p + b0, sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
+    if (sh->nsub) {   // one batch (ppg_shard_set_split checks): sub-jobs, then one result per chunk
+        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
+                                  sh->sjobs.p, sh->dicts.p, sh->out.p, sh->sres.p, (int)sh->h_sjobs.size(),
+                                  sh->snls.p));
+        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->sidx.p, sh->snls.p, sh->jobs.p, sh->res.p,
+                                      sh->nls.p, nb));
+    } else {
+        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
+                                  sh->jobs.p + b0, sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
+    }
     HIPCHK(hipEventRecord(sh->ev[1], s));
     HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
                                   sh->info.p + b0, sh->base.p + b0, sh->total.p, nb));
@@ -636,6 +661,85 @@ int ppg_shard_run(ppg_shard *sh) {
         if (rc != PPG_OK) return rc;
     }
     return shard_finish(sh, total_ms);
+}
+
+// Side points: deflate block starts strictly inside the shard's chunks (absolute file bit,
+// absolute output offset, the 32 KiB of output before it).  Chunk k is then decoded by one wave
+// per piece between its Point, its side points and the next Point; results are identical.
+int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
+                        const uint8_t *windows) {
+    if (!sh || nsub < 0 || (nsub && (!bit || !output || !windows))) return PPG_ARG_ERROR;
+    if (nsub && sh->batches.size() != 1) return PPG_UNSUPPORTED;   // sub-jobs need the whole shard resident
+    HIPCHK(hipSetDevice(sh->ctx->device));
+    hipStream_t s = shard_stream(sh);
+    const int32_t n = sh->n;
+    const std::vector<int64_t> &PO = sh->h_pout;
+    const int64_t base_byte = sh->base_byte;
+    // validate: sorted, strictly inside a chunk of the shard, bit inside that chunk's slice
+    std::vector<uint32_t> hidx((size_t)n + 1, 0);
+    {
+        int32_t c = 0;
+        for (int32_t t = 0; t < nsub; t++) {
+            if (t && output[t] <= output[t - 1]) return PPG_ARG_ERROR;
+            while (c < n && output[t] >= PO[(size_t)c + 1]) c++;
+            if (c >= n || output[t] <= PO[(size_t)c]) return PPG_ARG_ERROR;
+            const PpgInflateJob &J = sh->h_jobs[(size_t)c];
+            const int64_t rb = bit[t] - 8 * base_byte;
+            if (rb <= (int64_t)J.bit_start || rb >= (int64_t)J.bit_limit) return PPG_ARG_ERROR;
+            hidx[(size_t)c + 1]++;
+        }
+    }
+    sh->nsub = 0;
+    sh->ran = 0;
+    if (!nsub) return PPG_OK;
+    for (int32_t k = 0; k < n; k++) hidx[(size_t)k + 1] += hidx[(size_t)k] + 1;   // + the chunk's own first piece
+    uint64_t nl_bytes = kNlBytesPerEntry;
+    if (const char *e = getenv("PPG_NL_BYTES")) nl_bytes = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    sh->h_sjobs.assign((size_t)n + (size_t)nsub, PpgInflateJob{});
+    uint64_t nl_tot = 0;
+    int32_t t = 0;
+    for (int32_t k = 0; k < n; k++) {
+        const PpgInflateJob &C = sh->h_jobs[(size_t)k];
+        const int64_t from_out = PO[(size_t)k];
+        for (uint32_t j = hidx[(size_t)k]; j < hidx[(size_t)k + 1]; j++) {
+            PpgInflateJob J = C;
+            int64_t lo = 0;   // chunk-relative start of this piece
+            if (j > hidx[(size_t)k]) {
+                const int32_t q = t++;
+                lo = output[q] - from_out;
+                J.bit_start = (uint64_t)(bit[q] - 8 * base_byte);
+                J.dict_off = ((uint64_t)n + (uint64_t)q) * kWin;
+                J.raw_shift = C.raw_shift + (uint32_t)lo;
+                J.prev_byte = windows[(size_t)q * kWin + kWin - 1];
+            }
+            const int64_t hi = j + 1 < hidx[(size_t)k + 1] ? output[t] - from_out : (int64_t)C.out_len;
+            J.out_off = C.out_off + (uint64_t)lo;
+            J.out_len = (uint64_t)(hi - lo);
+            J.expect_end = ~0ull;
+            const uint64_t cap = nl_bytes >= (1ull << 40) ? 0 : J.out_len / nl_bytes + 64;
+            J.nl_off = nl_tot;
+            J.nl_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFu);
+            nl_tot += J.nl_cap;
+            sh->h_sjobs[j] = J;
+        }
+    }
+    // dictionaries: the chunks' windows, then the side points'
+    DevBuf<uint8_t> d2;
+    HIPCHK(d2.alloc(((size_t)n + (size_t)nsub) * kWin));
+    HIPCHK(hipMemcpyAsync(d2.p, sh->dicts.p, (size_t)n * kWin, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(d2.p + (size_t)n * kWin, windows, (size_t)nsub * kWin, hipMemcpyHostToDevice, s));
+    std::swap(sh->dicts.p, d2.p);
+    std::swap(sh->dicts.n, d2.n);
+    HIPCHK(sh->sjobs.alloc(sh->h_sjobs.size()));
+    HIPCHK(hipMemcpyAsync(sh->sjobs.p, sh->h_sjobs.data(), sizeof(PpgInflateJob) * sh->h_sjobs.size(),
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(sh->sres.alloc(sh->h_sjobs.size()));
+    HIPCHK(sh->sidx.alloc(hidx.size()));
+    HIPCHK(hipMemcpyAsync(sh->sidx.p, hidx.data(), 4 * hidx.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(sh->snls.alloc((size_t)nl_tot + 64));
+    HIPCHK(hipStreamSynchronize(s));   // staging vectors and d2 (the old dictionaries) die here
+    sh->nsub = nsub;
+    return PPG_OK;
 }
 
 int ppg_shard_results(ppg_shard *sh, int64_t *records, int64_t *produced, int32_t *status, int32_t *flags,

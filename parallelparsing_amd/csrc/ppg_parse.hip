@@ -9,6 +9,8 @@
 //   ppg_parse_emit    descriptors by scanning the body (chunks whose census overflowed nl_cap)
 //   ppg_record_keys   per-record spot ("major") number from the identifier line, for pairing
 //                     the two files of a read pair
+//   ppg_split_merge   chunks decoded as several sub-jobs (ppg_shard_set_split): one chunk result
+//                     and one contiguous newline census per chunk, as if one wave had decoded it
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "ppg_device.h"
@@ -251,6 +253,53 @@ extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
 }
 
 // ------------------------------------------------------------------------------------------
+// Split chunks (ppg_shard_set_split): chunk k was decoded as sub-jobs [sidx[k], sidx[k+1]) that
+// start at deflate block boundaries inside it, each with its own 32 KiB history.  Their results
+// are folded into the chunk's (in order: the first failing sub-job's status; every sub-job but
+// the last must produce exactly its bytes and end exactly where the next one starts), and their
+// stored newline positions -- already chunk-relative raw indices -- are concatenated into the
+// chunk's own census region, so the parse kernels see the chunk as one job.  One block per chunk.
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void ppg_split_merge(const PpgInflateJob *__restrict__ sjobs,
+                                                                  const PpgInflateResult *__restrict__ sres,
+                                                                  const uint32_t *__restrict__ sidx,
+                                                                  const uint32_t *__restrict__ snls,
+                                                                  const PpgInflateJob *__restrict__ jobs,
+                                                                  PpgInflateResult *__restrict__ res,
+                                                                  uint32_t *__restrict__ nls, int n) {
+    const int k = blockIdx.x;
+    if (k >= n) return;
+    const uint32_t s0 = sidx[k], s1 = sidx[k + 1];
+    const PpgInflateJob &C = jobs[k];
+    PpgInflateResult m = {};
+    uint32_t nl = 0;
+    for (uint32_t j = s0; j < s1; j++) {
+        const PpgInflateResult r = sres[j];
+        const bool tail = j + 1 == s1;
+        if (m.status == 0 && r.status != 0) m.status = r.status;
+        if (m.status == 0 && !tail && (r.produced != sjobs[j].out_len || r.end_bit != sjobs[j + 1].bit_start))
+            m.status = -3;   // Z_DATA_ERROR: the side point is not where this sub-job's blocks end
+        m.produced += r.produced;
+        m.flags |= tail ? r.flags : (r.flags & ~PPG_FLAG_NO_EOB);
+        m.pflags |= r.pflags;
+        m.nblocks += r.nblocks;
+        if (tail) { m.end_bit = r.end_bit; m.last = r.last; }
+        // positions of this sub-job, stored while its own capacity lasted
+        const uint32_t cnt = r.newlines;
+        if (!(m.pflags & PPG_PF_OVERFLOW) && nl + cnt <= C.nl_cap) {
+            const uint32_t *src = snls + sjobs[j].nl_off;
+            uint32_t *dst = nls + C.nl_off + nl;
+            for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) dst[i] = src[i];
+        } else {
+            m.pflags |= PPG_PF_OVERFLOW;
+        }
+        nl += cnt;
+    }
+    m.newlines = nl;
+    if (threadIdx.x == 0) res[k] = m;
+}
+
+// ------------------------------------------------------------------------------------------
 // Host-side launchers (called from ppg_api.cpp).
 // ------------------------------------------------------------------------------------------
 // after the inflate launch: per-chunk counts (census, or the serial machine) and their scan
@@ -283,5 +332,13 @@ hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgIn
                                   int n) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(ppg_record_keys, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, keys, n);
+    return hipGetLastError();
+}
+
+hipError_t ppg_launch_split_merge(hipStream_t s, const PpgInflateJob *sjobs, const PpgInflateResult *sres,
+                                  const uint32_t *sidx, const uint32_t *snls, const PpgInflateJob *jobs,
+                                  PpgInflateResult *res, uint32_t *nls, int n) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_split_merge, dim3(n), dim3(256), 0, s, sjobs, sres, sidx, snls, jobs, res, nls, n);
     return hipGetLastError();
 }

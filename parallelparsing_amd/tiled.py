@@ -85,6 +85,39 @@ class TiledFile:
                                      C.c_void_p(offs.ctypes.data))
         return win, offs[: int(self.p_offlen[lo:hi].sum())]
 
+    def side_points(self, lo=0, hi=None, per_chunk=2):
+        """Side points for Shard.set_split over points [lo, hi): up to per_chunk - 1 deflate block
+        starts inside each chunk, spread evenly by output.  (bits, outputs, windows) with absolute
+        file bit positions and output offsets, windows = the 32 KiB of text before each."""
+        if hi is None:
+            hi = self.npoints
+        po = self.p_output[lo:hi]
+        if per_chunk < 2 or po.size < 2:
+            return np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.uint8)
+        tl, segbits = self.text.size, 8 * self.seg.size
+        frac = np.arange(1, per_chunk, dtype=np.float64) / per_chunk
+        tgt = (po[:-1, None] + (np.diff(po)[:, None] * frac[None, :])).astype(np.int64).ravel()
+        # first block end at or after each target (block ends repeat every segment)
+        r = tgt // tl
+        b = np.searchsorted(self.block_out_end, tgt - r * tl, side="left")
+        wrap = b >= self.block_out_end.size
+        r, b = np.where(wrap, r + 1, r), np.where(wrap, 0, b)
+        outs = r * tl + self.block_out_end[b]
+        bits = 80 + r * segbits + self.block_bit_end[b]
+        # strictly inside their chunk, one per block end
+        c = np.repeat(np.arange(po.size - 1), per_chunk - 1)
+        keep = (outs > po[c]) & (outs < po[c + 1])
+        outs, bits = outs[keep], bits[keep]
+        outs, first = np.unique(outs, return_index=True)
+        bits = bits[first]
+        win = np.empty(outs.size * 32768, np.uint8)
+        z32, z64 = np.zeros(max(1, outs.size), np.int32), np.zeros(max(1, outs.size), np.int64)
+        if outs.size:
+            synth().ppg_synth_tiled_fill(C.c_void_p(self.text.ctypes.data), tl, C.c_void_p(outs.ctypes.data),
+                                         C.c_void_p(z32.ctypes.data), C.c_void_p(z64.ctypes.data), 0, outs.size,
+                                         C.c_void_p(win.ctypes.data), C.c_void_p(z64.ctypes.data))
+        return bits.astype(np.int64), outs.astype(np.int64), win
+
     @property
     def text_len(self):
         return self.text.size

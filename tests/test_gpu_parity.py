@@ -214,3 +214,126 @@ def test_census_capacity_extremes(nl_bytes, device, monkeypatch):
             assert len(rec) == c["records"], (name, k)
             assert sha(np.ascontiguousarray(rec, "<u4").tobytes()) == c["rec_sha256"], (name, k)
         assert sh.total_records == meta["total_records"]
+
+
+def dense_side_points(gz, ix, chunksize=9):
+    """Side points for ppg_shard_set_split from the oracle's CreateIndex at a tiny chunk size (a
+    Point at almost every block end, with its window): those strictly inside ix's chunks."""
+    dx = O.build_index(gz, chunksize)
+    outs = np.array([ix.point_fields(k)[0] for k in range(ix.Count)], np.int64)
+    bits, out, wins = [], [], []
+    for o, n, b, w, _ in dx.points():
+        c = int(np.searchsorted(outs, o, side="right")) - 1
+        if 0 <= c < ix.Count - 1 and outs[c] < o < outs[c + 1]:
+            bits.append(8 * n - b)
+            out.append(o)
+            wins.append(np.frombuffer(w, np.uint8))
+    win = np.concatenate(wins) if wins else np.zeros(0, np.uint8)
+    return np.array(bits, np.int64), np.array(out, np.int64), win
+
+
+def assert_same_run(a, b, n):
+    ra, rb = a.results(), b.results()
+    for key in ra:
+        assert (ra[key] == rb[key]).all(), key
+    assert a.total_records == b.total_records
+    assert (a.record_base() == b.record_base()).all()
+    for k in range(n):
+        assert sha(a.chunk_bytes(k)) == sha(b.chunk_bytes(k)), k
+        assert (a.chunk_records(k) == b.chunk_records(k)).all(), k
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_split_chunks_match_golden(name, device):
+    """Chunks decoded as several waves (side points at inner block starts, ppg_shard_set_split)
+    give exactly the golden bytes and record tables, and the same results as one wave per chunk."""
+    meta, gz = load_case(name)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    n = ix.Count - 1
+    bits, outs, win = dense_side_points(gz, ix)
+    one = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).set_split(bits, outs, win).run()
+    for k, c in enumerate(meta["chunks"]):
+        assert sha(sh.chunk_bytes(k)) == c["sha256"], (name, k)
+        assert sha(np.ascontiguousarray(sh.chunk_records(k), "<u4").tobytes()) == c["rec_sha256"], (name, k)
+    assert_same_run(one, sh, n)
+    # and back to one wave per chunk
+    sh.set_split([], [], np.zeros(0, np.uint8)).run()
+    assert_same_run(one, sh, n)
+
+
+@pytest.mark.parametrize("per", [2, 3, 8])
+def test_split_tiled_member(per, device):
+    """bench.py's --split path: TiledFile.side_points over a small tiled member."""
+    from parallelparsing_amd.tiled import TiledFile
+    tf = TiledFile(3000, 6, 1000, threads=4)
+    f = tf.file_bytes()
+    ix = tf.index()
+    n = tf.npoints - 1
+    one = pp.Shard(ix, comp_range(f, ix, 0, n), 0, n, device=device).run()
+    bits, outs, win = tf.side_points(per_chunk=per)
+    assert bits.size > n // 2
+    sh = pp.Shard(ix, comp_range(f, ix, 0, n), 0, n, device=device).set_split(bits, outs, win).run()
+    assert_same_run(one, sh, n)
+    assert sh.total_records == tf.expected_records()
+    text = tf.text.tobytes() * tf.repeats
+    for k in range(n):
+        assert sh.chunk_bytes(k).tobytes() == text[tf.p_output[k]:tf.p_output[k + 1]], k
+
+
+@pytest.mark.parametrize("nl_bytes", ["1099511627776", "1"])
+def test_split_census_capacity_extremes(nl_bytes, device, monkeypatch):
+    monkeypatch.setenv("PPG_NL_BYTES", nl_bytes)
+    for name in ["l6_c200", "crlf_c100", "fixed_c100"]:
+        meta, gz = load_case(name)
+        ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+        n = ix.Count - 1
+        bits, outs, win = dense_side_points(gz, ix)
+        sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).set_split(bits, outs, win).run()
+        for k, c in enumerate(meta["chunks"]):
+            assert sha(np.ascontiguousarray(sh.chunk_records(k), "<u4").tobytes()) == c["rec_sha256"], (name, k)
+        assert sh.total_records == meta["total_records"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_split_whole_member_chunk(name, device):
+    """One chunk spanning the member (CreateIndex at a chunk size no file reaches), split at every
+    inner block end: the bytes are the member's text, the records the oracle's DecompressAll, and
+    both equal the one-wave run -- covers every golden case (fixed, stored, CRLF, NUL, malformed)."""
+    meta, gz = load_case(name)
+    big = 1 << 30
+    ix = pp.Core.BuildDeflateIndex(gz, big)
+    n = ix.Count - 1
+    bits, outs, win = dense_side_points(gz, ix)
+    one = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).set_split(bits, outs, win).run()
+    assert_same_run(one, sh, n)
+    text = zlib.decompress(gz, 47)
+    assert b"".join(sh.chunk_bytes(k).tobytes() for k in range(n)) == text
+    tot, _ = O.decompress_all(gz, O.build_index(gz, big), threads=4)
+    assert sh.total_records == tot
+
+
+def test_split_rejects_bad_side_points(device):
+    meta, gz = load_case("memlevel1_c10")
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    n = ix.Count - 1
+    bits, outs, win = dense_side_points(gz, ix)
+    assert bits.size >= 2
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device)
+    with pytest.raises(RuntimeError):   # not sorted
+        sh.set_split(bits[::-1].copy(), outs[::-1].copy(), win)
+    with pytest.raises(RuntimeError):   # on a chunk Point, not strictly inside a chunk
+        o0 = ix.point_fields(1)[0]
+        sh.set_split(bits[:1], np.array([o0], np.int64), win[:32768])
+    # a side point one byte late: the piece before it cannot end there
+    sh.set_split(bits[:1], outs[:1] + 1, win[:32768])
+    with pytest.raises(RuntimeError):
+        sh.run()
+    r = sh.results()
+    assert (r["status"] != 0).sum() == 1
+    # batched shards cannot be split
+    b = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device, out_capacity=8192)
+    if b.batches > 1:
+        with pytest.raises(RuntimeError):
+            b.set_split(bits, outs, win)

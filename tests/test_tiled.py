@@ -41,3 +41,29 @@ def test_tiled_points_equal_oracle(records, repeats, chunk, piece):
     assert w2.tobytes() == win[lo * 32768:hi * 32768].tobytes()
     s0 = int(tf.p_offlen[:lo].sum())
     assert o2.tobytes() == offs[s0:s0 + len(o2)].tobytes()
+
+
+@pytest.mark.parametrize("records,repeats,chunk,per", [(3000, 5, 1000, 3), (2500, 4, 5000, 8)])
+def test_side_points_are_block_starts(records, repeats, chunk, per):
+    """TiledFile.side_points (ppg_shard_set_split's input in bench.py): every side point is a deflate
+    block start inside a chunk whose window is the text before it -- the oracle's Core.Extract from
+    an index of chunk Points + side points reproduces the text piece by piece."""
+    tf = TiledFile(records, repeats, chunk, threads=4)
+    f = tf.file_bytes().tobytes()
+    text = tf.text.tobytes() * repeats
+    bits, outs, win = tf.side_points(per_chunk=per)
+    assert bits.size > 0 and np.all(np.diff(outs) > 0)
+    c = np.searchsorted(tf.p_output, outs, side="right") - 1
+    assert np.all(outs > tf.p_output[c]) and np.all(outs < tf.p_output[c + 1])
+    assert np.bincount(c).max() <= per - 1
+    cw, _ = tf.windows()
+    o = np.concatenate([tf.p_output, outs])
+    b = np.concatenate([8 * tf.p_input - tf.p_bits, bits])
+    w = np.concatenate([cw.reshape(-1, 32768), win.reshape(-1, 32768)])
+    order = np.argsort(o, kind="stable")
+    o, b, w = o[order], b[order], w[order]
+    inp = (b + 7) // 8
+    ix = O.index_from_points(o, inp, inp * 8 - b, w.ravel(), np.zeros(o.size, np.int32), b"")
+    for k in range(o.size - 1):
+        assert O.extract(f, ix, k) == text[o[k]:o[k + 1]], k
+        assert w[k].tobytes() == (b"\0" * 32768 + text[:o[k]])[-32768:], k
