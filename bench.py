@@ -195,6 +195,7 @@ def paired_run(args, dev):
     # one ctx (= one HIP stream) per file, so the two DecompressAll passes run concurrently: at
     # chunk = 50,000 one file has only ~2.7k chunks, a third of the GPU's 8k wave slots
     ctxs = [pp.Device(dev.index), pp.Device(dev.index)]
+    args.split = auto_split(args, dev, sum(tf.npoints - 1 for tf in tfs))
     shards, bufs = [], []
     for tf, ctx in zip(tfs, ctxs):
         lo, hi = int(tf.p_input[0]) - 1, int(tf.p_input[-1])
@@ -205,6 +206,8 @@ def paired_run(args, dev):
         out_cap = int(tf.p_output[-1] - tf.p_output[0]) + (1 << 20)
         shards.append(pp.Shard(tf.index(0, tf.npoints), comp.data_ptr(), first=0, n=tf.npoints - 1, device=ctx,
                                comp_on_device=True, comp_len=hi - lo, out_capacity=out_cap))
+        if args.split > 1:
+            shards[-1].set_split(*tf.side_points(0, tf.npoints, args.split))
     torch.cuda.synchronize()
 
     import threading
@@ -243,9 +246,22 @@ def paired_run(args, dev):
         "data": "synthetic (Generator-shape 150 bp read pairs, tiled single gzip members, zlib level 6)",
         "config": {"workload": f"configs[4]-shaped: 2 x {tfs[0].file_len / 1e9:.1f} GB .fastq.gz on one GPU, "
                                f"chunk=50000, pair chunks of 50,000 records",
-                   "pairs": npairs, "gz_bytes": [tf.file_len for tf in tfs], "decompressed_bytes": text},
+                   "pairs": npairs, "gz_bytes": [tf.file_len for tf in tfs], "decompressed_bytes": text,
+                   "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
         "decompressed_MBps": text * args.steps / elapsed / 1e6,
     }
+
+
+def auto_split(args, dev, chunks):
+    """--split 0: one wave per chunk while a rank holds >= ~6 generations of resident waves (CUs x
+    32), else up to 16 waves per chunk.  Measured on one MI355X: a strong-scaled rank
+    at N = 8 (6.8k chunks) 149.9 -> 119.4 ms with 8, N = 4 251.7 -> 230.6 ms with 4; the full
+    52.7k-chunk step is not helped (885 vs 890 ms with 2)."""
+    if args.split > 0:
+        return args.split
+    import torch
+    slots = torch.cuda.get_device_properties(dev).multi_processor_count * 32
+    return int(min(16, max(1, -(-6 * slots // max(1, chunks)))))
 
 
 def main():
@@ -267,6 +283,11 @@ def main():
     ap.add_argument("--paired", action="store_true",
                     help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
     ap.add_argument("--paired-repeats", type=int, default=51)   # ~12.5 GB gz per file
+    ap.add_argument("--split", type=int, default=0,
+                    help="decode each chunk as up to S waves, split at inner deflate block starts "
+                         "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
+                         "0 (default) = auto: enough waves for ~6 generations of the GPU's wave slots (S = 1 for "
+                         "the default 50 GB-per-GPU workload, 8 for a strong-scaled rank at N = 8)")
     ap.add_argument("--ingest", action="store_true",
                     help="also time DecompressAll straight from the .gz file on disk (host ingest, PCIe-inclusive; "
                          "reported under 'ingest', never as value)")
@@ -310,6 +331,11 @@ def main():
     out_cap = int(args.out_capacity_gib * (1 << 30))
     shard = pp.Shard(index, comp.data_ptr(), first=0, n=b - a, device=ctx, comp_on_device=True, comp_len=comp_len,
                      out_capacity=out_cap)
+    args.split = auto_split(args, dev, b - a)
+    if args.split > 1:
+        sb, so, sw = tf.side_points(a, b + 1, args.split)
+        shard.set_split(sb, so, sw)
+        log(f"[bench] rank {rank}: split into {b - a + sb.size} waves ({sb.size} side points)")
     log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
         f"{shard.batches} output batch(es), setup {time.time() - t:.1f}s")
     counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
@@ -381,7 +407,8 @@ def main():
         "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)",
         "config": {"workload": workload,
                    "records": total_records, "gz_bytes": tf.file_len, "decompressed_bytes": text_bytes,
-                   "chunks": nchunks, "parallelism": f"chunk-sharded x{world}"},
+                   "chunks": nchunks, "parallelism": f"chunk-sharded x{world}",
+                   "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
         "decompressed_MBps": text_bytes * args.steps / elapsed / 1e6,
         "kernel_ms_per_step": {"inflate": infl_ms / args.steps, "parse": parse_ms / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
