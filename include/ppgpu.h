@@ -62,6 +62,17 @@ int ppg_index_build_mem(const uint8_t *gz, int64_t gz_len, uint32_t chunksize, p
  * Returns PPG_UNSUPPORTED for zlib-wrapped / multi-member input (use ppg_index_build_file). */
 int ppg_index_build_gpu(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
                         int64_t piece_bytes, int64_t out_capacity, ppg_index **out);
+
+/* ppg_index_build_gpu that also records side points for ppg_shard_set_split: at every block end
+ * at least side_bytes of output past the previous Point or side point (and not itself a Point),
+ * its absolute bit, output offset and 32 KiB window, gathered on the GPU while the batch's output
+ * is resident.  side_bytes <= 0: none.  Side points are not part of the .gzi (IndexIO). */
+int ppg_index_build_gpu_side(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
+                             int64_t piece_bytes, int64_t out_capacity, int64_t side_bytes, ppg_index **out);
+int ppg_index_side_count(const ppg_index *ix);
+/* copies the side points (any pointer may be NULL): count entries, windows count * 32768 bytes */
+int ppg_index_side_points(const ppg_index *ix, int64_t *bit, int64_t *output, uint8_t *windows);
+
 int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksize, int64_t piece_bytes,
                              ppg_index **out);
 /* Last GPU CreateIndex on ctx: [0] finder ms, [1] pass-1 ms, [2] chain check ms, [3] pass-2 ms,

@@ -97,6 +97,19 @@ class Index:
             return np.zeros(0, np.uint8)
         return np.frombuffer(C.string_at(lib.ppg_index_window(self._h, 0), n * WINSIZE), np.uint8)
 
+    def side_points(self, first=0, n=None):
+        """(bits, outputs, windows) of the side points BuildDeflateIndexGpu(side_bytes=...) recorded,
+        those inside chunks [first, first+n) (a Shard's range) -- Shard.set_split's arguments."""
+        m = lib.ppg_index_side_count(self._h)
+        bits, outs = np.zeros(max(1, m), np.int64), np.zeros(max(1, m), np.int64)
+        win = np.zeros(max(1, m) * 32768, np.uint8)
+        check(lib.ppg_index_side_points(self._h, _ptr(bits), _ptr(outs), _ptr(win)), "side_points")
+        if n is None:
+            n = self.Count - 1 - first
+        lo, hi = self.point_fields(first)[0], self.point_fields(first + n)[0]
+        keep = np.nonzero((outs[:m] > lo) & (outs[:m] < hi))[0]
+        return bits[keep], outs[keep], win.reshape(-1, 32768)[keep].ravel()
+
     @staticmethod
     def from_points(output, inp, bits, windows, offset_len, offsets, chunk_max_bytes=0):
         """Index from arrays (ppg_index_from_points): windows is count*32768 bytes."""
@@ -244,23 +257,27 @@ class Core:
         return Index(h.value)
 
     @staticmethod
-    def BuildDeflateIndexGpu(gz, chunksize, device=None, piece_bytes=0, out_capacity=0):
+    def BuildDeflateIndexGpu(gz, chunksize, device=None, piece_bytes=0, out_capacity=0, side_bytes=0):
         """CreateIndex on the GPU (ppg_index_gpu.cpp): the same Points as BuildDeflateIndex for a
         single-member gzip, from a block-parallel decode.  gz: a path, bytes / uint8 array (host),
         or a uint8 torch tensor on the device.  Raises PpgError(PPG_UNSUPPORTED) for zlib-wrapped
-        or multi-member input (BuildDeflateIndex handles those)."""
+        or multi-member input (BuildDeflateIndex handles those).  side_bytes > 0 (in-memory input)
+        also records side points every >= side_bytes of output inside chunks (Index.side_points,
+        for Shard.set_split)."""
         dev = device or Device.default()
         h = C.c_void_p()
         cs = int(chunksize) & 0xFFFFFFFF
         if isinstance(gz, (str, os.PathLike)):
+            if side_bytes:
+                raise ValueError("side_bytes needs the member in memory (host or device)")
             rc = lib.ppg_index_build_gpu_file(dev.handle, os.fsencode(gz), cs, int(piece_bytes), C.byref(h))
         elif hasattr(gz, "data_ptr"):
-            rc = lib.ppg_index_build_gpu(dev.handle, C.c_void_p(gz.data_ptr()), gz.numel(), 1, cs, int(piece_bytes),
-                                         int(out_capacity), C.byref(h))
+            rc = lib.ppg_index_build_gpu_side(dev.handle, C.c_void_p(gz.data_ptr()), gz.numel(), 1, cs,
+                                              int(piece_bytes), int(out_capacity), int(side_bytes), C.byref(h))
         else:
             a = _as_u8(gz)
-            rc = lib.ppg_index_build_gpu(dev.handle, _ptr(a), a.size, 0, cs, int(piece_bytes), int(out_capacity),
-                                         C.byref(h))
+            rc = lib.ppg_index_build_gpu_side(dev.handle, _ptr(a), a.size, 0, cs, int(piece_bytes),
+                                              int(out_capacity), int(side_bytes), C.byref(h))
         check(rc, "Core.BuildDeflateIndexGpu")
         return Index(h.value)
 

@@ -66,6 +66,9 @@ _SIGS = {
     "ppg_index_build_file": (C.c_int, [C.c_char_p, u32, P(vp)]),
     "ppg_index_build_mem": (C.c_int, [vp, i64, u32, P(vp)]),
     "ppg_index_build_gpu": (C.c_int, [vp, vp, i64, C.c_int, u32, i64, i64, P(vp)]),
+    "ppg_index_build_gpu_side": (C.c_int, [vp, vp, i64, C.c_int, u32, i64, i64, i64, P(vp)]),
+    "ppg_index_side_count": (C.c_int, [vp]),
+    "ppg_index_side_points": (C.c_int, [vp, vp, vp, vp]),
     "ppg_index_build_gpu_file": (C.c_int, [vp, C.c_char_p, u32, i64, P(vp)]),
     "ppg_index_build_gpu_stats": (C.c_int, [vp, P(C.c_double), i32]),
     "ppg_index_serialize": (C.c_int, [vp, C.c_char_p]),

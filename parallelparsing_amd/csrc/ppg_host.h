@@ -42,6 +42,10 @@ struct ppg_index {
     // contiguous array, so a range of chunks ships its windows to the GPU in one copy
     std::vector<uint8_t> windows;
     const uint8_t *win(size_t i) const { return windows.data() + i * kWin; }
+    // side points (ppg_index_build_gpu_side; not part of the .gzi): block starts inside chunks,
+    // absolute bit / output and their 32 KiB windows, for ppg_shard_set_split
+    std::vector<int64_t> side_bit, side_out;
+    std::vector<uint8_t> side_win;
 
     // Index.AddPoint (Common/Index.cs:24-48)
     void add_point(int bits, int64_t input, int64_t output, uint32_t left, const uint8_t *circ,

@@ -199,7 +199,7 @@ struct Builder {
 
 static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, const uint8_t *head, int64_t head_n,
                            const uint8_t trailer[8], uint32_t chunksize, int64_t piece_bytes, int64_t out_capacity,
-                           ppg_index &ix) {
+                           int64_t side_bytes, ppg_index &ix) {
     const auto t_all = Clock::now();
     double *stat = ctx->ix_stats;
     std::fill(stat, stat + 16, 0.0);
@@ -393,7 +393,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
 
     // Core.cs:79-110 state carried across batches
     const int64_t threshold = (int64_t)(uint32_t)(chunksize - 8u);
-    int64_t records = 0, last_at = -1;
+    int64_t records = 0, last_at = -1, last_mark = 0;   // last_mark: output of the last Point or side point
     int batches = 0;
     uint64_t nblocks_seen = 0;
     double t_census = 0;
@@ -471,6 +471,8 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         const bool final_batch = b1 == np;
         struct Pick { int64_t bits, input, output; uint32_t j; uint64_t rel; int64_t off_len; };
         std::vector<Pick> picks;
+        struct Side { uint64_t end_bit; int64_t output; uint32_t j; uint64_t rel; };
+        std::vector<Side> sides;
         for (size_t i = 0; i < refs.size(); i++) {
             const BlockRef &br = refs[i];
             const uint64_t gs = O[br.j] + (hs[i].lo - h2[br.j].out_off);
@@ -492,6 +494,19 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
                 if (off_len > kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
                 picks.push_back(Pick{bits, input, (int64_t)ge, br.j, br.rel_end, off_len});
                 records = 0;
+                last_mark = (int64_t)ge;
+                // a side point at this output (an empty block before this one) would not be inside a chunk
+                if (!sides.empty() && sides.back().output == (int64_t)ge) sides.pop_back();
+                if (sides.empty() && !ix.side_out.empty() && ix.side_out.back() == (int64_t)ge) {
+                    ix.side_bit.pop_back();
+                    ix.side_out.pop_back();
+                    ix.side_win.resize(ix.side_win.size() - kWin);
+                }
+            } else if (side_bytes > 0 && (int64_t)ge - last_mark >= side_bytes &&
+                       (sides.empty() || sides.back().output != (int64_t)ge)) {
+                // a side point: a block start inside the current chunk, side_bytes past the last mark
+                sides.push_back(Side{br.end_bit, (int64_t)ge, br.j, br.rel_end});
+                last_mark = (int64_t)ge;
             }
         }
         nblocks_seen += refs.size();
@@ -499,6 +514,8 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         std::vector<PpgGather> gw;
         for (const Pick &p : picks)
             if (p.output > 0) gw.push_back(PpgGather{h2[p.j].out_off, (uint64_t)p.j * kWin, p.rel, ~0ull, 0});
+        const size_t npick_w = gw.size();
+        for (const Side &d : sides) gw.push_back(PpgGather{h2[d.j].out_off, (uint64_t)d.j * kWin, d.rel, ~0ull, 0});
         std::vector<uint8_t> hw(gw.size() * kWin);
         if (!gw.empty()) {
             HIPCHK(B.gat.alloc(gw.size()));
@@ -507,6 +524,12 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, dwin.p, nullptr, nullptr, (int)gw.size()));
             HIPCHK(hipMemcpyAsync(hw.data(), dwin.p, hw.size(), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
+        }
+        for (size_t i = 0; i < sides.size(); i++) {
+            ix.side_bit.push_back((int64_t)sides[i].end_bit);
+            ix.side_out.push_back(sides[i].output);
+            const uint8_t *w = hw.data() + (npick_w + i) * kWin;
+            ix.side_win.insert(ix.side_win.end(), w, w + kWin);
         }
         size_t wi = 0;
         for (const Pick &p : picks) {
@@ -551,8 +574,27 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
 
 extern "C" {
 
+int ppg_index_build_gpu_side(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
+                             int64_t piece_bytes, int64_t out_capacity, int64_t side_bytes, ppg_index **out);
+
 int ppg_index_build_gpu(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
                         int64_t piece_bytes, int64_t out_capacity, ppg_index **out) {
+    return ppg_index_build_gpu_side(ctx, gz, gz_len, gz_on_device, chunksize, piece_bytes, out_capacity, 0, out);
+}
+
+int ppg_index_side_count(const ppg_index *ix) { return ix ? (int)ix->side_out.size() : -1; }
+
+int ppg_index_side_points(const ppg_index *ix, int64_t *bit, int64_t *output, uint8_t *windows) {
+    if (!ix) return PPG_ARG_ERROR;
+    const size_t n = ix->side_out.size();
+    if (bit) std::copy(ix->side_bit.begin(), ix->side_bit.end(), bit);
+    if (output) std::copy(ix->side_out.begin(), ix->side_out.end(), output);
+    if (windows && n) memcpy(windows, ix->side_win.data(), n * kWin);
+    return PPG_OK;
+}
+
+int ppg_index_build_gpu_side(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
+                             int64_t piece_bytes, int64_t out_capacity, int64_t side_bytes, ppg_index **out) {
     if (!ctx || !gz || gz_len <= 0 || !out) return PPG_ARG_ERROR;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -575,7 +617,8 @@ int ppg_index_build_gpu(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_
         d = own.p;
     }
     auto ix = std::make_unique<ppg_index>();
-    const int rc = build_index_gpu(ctx, d, gz_len, head.data(), hn, trailer, chunksize, piece_bytes, out_capacity, *ix);
+    const int rc = build_index_gpu(ctx, d, gz_len, head.data(), hn, trailer, chunksize, piece_bytes, out_capacity,
+                                   side_bytes, *ix);
     if (rc != PPG_OK) return rc;
     *out = ix.release();
     return PPG_OK;
@@ -628,7 +671,7 @@ int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksi
     if (len >= 8 && pread(fd, trailer, 8, (off_t)(len - 8)) != 8) return PPG_IO_ERROR;
     auto ix = std::make_unique<ppg_index>();
     const double upload = ms_since(t0);
-    const int rc = build_index_gpu(ctx, dev.p, len, head.data(), hn, trailer, chunksize, piece_bytes, 0, *ix);
+    const int rc = build_index_gpu(ctx, dev.p, len, head.data(), hn, trailer, chunksize, piece_bytes, 0, 0, *ix);
     ctx->ix_stats[14] = upload;
     if (rc != PPG_OK) return rc;
     *out = ix.release();

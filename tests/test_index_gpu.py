@@ -191,3 +191,45 @@ def test_index_feeds_decompress_all(device):
     _, i1, _, _ = ix.point_fields(n)
     sh = pp.Shard(ix, gz[i0 - 1:i1], 0, n, device=device).run()
     assert sh.total_records == nrec
+
+
+@pytest.mark.parametrize("side,cap,pigz", [(300_000, 0, 0), (100_000, 3 << 20, 0), (200_000, 0, 128 << 10)])
+def test_side_points_split_decompress_all(side, cap, pigz, device):
+    """GPU CreateIndex with side points (ppg_index_build_gpu_side): the Points are unchanged, every
+    side point is a block start strictly inside a chunk whose window is the text before it, and
+    DecompressAll split at them (Shard.set_split) equals the one-wave run."""
+    nrec = 200_000
+    txt = fastq_text(nrec, seed=21)
+    gz = synth_gz(txt, level=6, piece=pigz)
+    ix = pp.Core.BuildDeflateIndexGpu(gz, 10000, device=device, out_capacity=cap, side_bytes=side)
+    same_index(ix, pp.Core.BuildDeflateIndex(gz, 10000))
+    bits, outs, win = ix.side_points()
+    n = ix.Count - 1
+    assert bits.size >= n   # chunks hold ~3.8 MB of text
+    po = np.array([ix.point_fields(k)[0] for k in range(ix.Count)])
+    c = np.searchsorted(po, outs, side="right") - 1
+    assert np.all(np.diff(outs) > 0) and np.all(outs > po[c]) and np.all(outs < po[c + 1])
+    assert np.all(np.diff(np.concatenate([po, outs]).astype(np.int64)[np.argsort(np.concatenate([po, outs]))])
+                  > 0)
+    t = txt.tobytes()
+    for i in range(0, outs.size, max(1, outs.size // 16)):
+        o = int(outs[i])
+        assert win[i * 32768:(i + 1) * 32768].tobytes() == (b"\0" * 32768 + t[:o])[-32768:], i
+    _, i0, _, _ = ix.point_fields(0)
+    _, i1, _, _ = ix.point_fields(n)
+    one = pp.Shard(ix, gz[i0 - 1:i1], 0, n, device=device).run()
+    sh = pp.Shard(ix, gz[i0 - 1:i1], 0, n, device=device).set_split(bits, outs, win).run()
+    ra, rb = one.results(), sh.results()
+    for key in ra:
+        assert (ra[key] == rb[key]).all(), key
+    assert sh.total_records == one.total_records == nrec
+    for k in range(n):
+        assert sh.chunk_bytes(k).tobytes() == t[po[k]:po[k + 1]], k
+        assert (sh.chunk_records(k) == one.chunk_records(k)).all(), k
+    # a shard over a sub-range takes the side points inside it
+    b2, o2, w2 = ix.side_points(2, 3)
+    assert b2.size and np.all((o2 > po[2]) & (o2 < po[5]))
+    _, j0, _, _ = ix.point_fields(2)
+    _, j1, _, _ = ix.point_fields(5)
+    s3 = pp.Shard(ix, gz[j0 - 1:j1], 2, 3, device=device).set_split(b2, o2, w2).run()
+    assert (s3.results()["records"] == ra["records"][2:5]).all()
