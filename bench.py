@@ -195,7 +195,7 @@ def paired_run(args, dev):
     # one ctx (= one HIP stream) per file, so the two DecompressAll passes run concurrently: at
     # chunk = 50,000 one file has only ~2.7k chunks, a third of the GPU's 8k wave slots
     ctxs = [pp.Device(dev.index), pp.Device(dev.index)]
-    args.split = auto_split(args, dev, sum(tf.npoints - 1 for tf in tfs))
+    args.split, _ = auto_split(args, dev, sum(tf.npoints - 1 for tf in tfs))
     shards, bufs = [], []
     for tf, ctx in zip(tfs, ctxs):
         lo, hi = int(tf.p_input[0]) - 1, int(tf.p_input[-1])
@@ -253,15 +253,18 @@ def paired_run(args, dev):
 
 
 def auto_split(args, dev, chunks):
-    """--split 0: one wave per chunk while a rank holds >= ~6 generations of resident waves (CUs x
-    32), else up to 16 waves per chunk.  Measured on one MI355X: a strong-scaled rank
-    at N = 8 (6.8k chunks) 149.9 -> 119.4 ms with 8, N = 4 251.7 -> 230.6 ms with 4; the full
-    52.7k-chunk step is not helped (885 vs 890 ms with 2)."""
+    """(S, K): split the last K of a rank's chunks into up to S waves each (ppg_shard_set_split).
+    --split S > 0: every chunk.  --split 0 (auto): a rank holding fewer than ~6 generations of
+    resident waves (CUs x 32) splits every chunk, into enough waves for ~6 generations (at most 16);
+    a larger rank splits only its last generation, into 4, so the launch's tail drains in a
+    quarter of a chunk's time.  Measured on one MI355X."""
     if args.split > 0:
-        return args.split
+        return args.split, chunks
     import torch
     slots = torch.cuda.get_device_properties(dev).multi_processor_count * 32
-    return int(min(16, max(1, -(-6 * slots // max(1, chunks)))))
+    if chunks < 6 * slots:
+        return int(min(16, max(1, -(-6 * slots // max(1, chunks))))), chunks
+    return args.tail_split, min(chunks, int(args.tail_gens * slots))
 
 
 def main():
@@ -283,6 +286,10 @@ def main():
     ap.add_argument("--paired", action="store_true",
                     help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
     ap.add_argument("--paired-repeats", type=int, default=51)   # ~12.5 GB gz per file
+    ap.add_argument("--tail-split", type=int, default=8,
+                    help="--split 0 on a large rank: waves per chunk for its last generation of chunks (1 = off)")
+    ap.add_argument("--tail-gens", type=float, default=0.5,
+                    help="--split 0 on a large rank: how many generations of its last chunks to split")
     ap.add_argument("--split", type=int, default=0,
                     help="decode each chunk as up to S waves, split at inner deflate block starts "
                          "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
@@ -331,11 +338,12 @@ def main():
     out_cap = int(args.out_capacity_gib * (1 << 30))
     shard = pp.Shard(index, comp.data_ptr(), first=0, n=b - a, device=ctx, comp_on_device=True, comp_len=comp_len,
                      out_capacity=out_cap)
-    args.split = auto_split(args, dev, b - a)
+    args.split, ksplit = auto_split(args, dev, b - a)
     if args.split > 1:
-        sb, so, sw = tf.side_points(a, b + 1, args.split)
+        sb, so, sw = tf.side_points(b - ksplit, b + 1, args.split)
         shard.set_split(sb, so, sw)
-        log(f"[bench] rank {rank}: split into {b - a + sb.size} waves ({sb.size} side points)")
+        log(f"[bench] rank {rank}: last {ksplit} chunks split, {b - a + sb.size} waves ({sb.size} side points)")
+    args.split_chunks = ksplit if args.split > 1 else 0
     log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
         f"{shard.batches} output batch(es), setup {time.time() - t:.1f}s")
     counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
@@ -408,7 +416,8 @@ def main():
         "config": {"workload": workload,
                    "records": total_records, "gz_bytes": tf.file_len, "decompressed_bytes": text_bytes,
                    "chunks": nchunks, "parallelism": f"chunk-sharded x{world}",
-                   "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
+                   "waves_per_chunk": (f"<= {args.split} for the last {args.split_chunks} chunks per rank "
+                                       f"(side points)") if args.split > 1 else 1},
         "decompressed_MBps": text_bytes * args.steps / elapsed / 1e6,
         "kernel_ms_per_step": {"inflate": infl_ms / args.steps, "parse": parse_ms / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -399,7 +399,6 @@ struct ppg_shard {
     DevBuf<PpgInflateJob> sjobs;
     DevBuf<PpgInflateResult> sres;
     DevBuf<uint32_t> sidx;                      // chunk k = sub-jobs [sidx[k], sidx[k+1])
-    DevBuf<uint32_t> snls;                      // the sub-jobs' own census regions
 };
 
 extern "C" {
@@ -577,8 +576,8 @@ static int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     if (sh->nsub) {   // one batch (ppg_shard_set_split checks): sub-jobs, then one result per chunk
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
                                   sh->sjobs.p, sh->dicts.p, sh->out.p, sh->sres.p, (int)sh->h_sjobs.size(),
-                                  sh->snls.p));
-        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->sidx.p, sh->snls.p, sh->jobs.p, sh->res.p,
+                                  sh->nls.p));
+        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->sidx.p, sh->nls.p, sh->jobs.p, sh->res.p,
                                       sh->nls.p, nb));
     } else {
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
@@ -696,11 +695,19 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     uint64_t nl_bytes = kNlBytesPerEntry;
     if (const char *e = getenv("PPG_NL_BYTES")) nl_bytes = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     sh->h_sjobs.assign((size_t)n + (size_t)nsub, PpgInflateJob{});
+    // census regions: a chunk left whole keeps its own region of sh->nls (nothing to merge); the
+    // pieces of a split chunk get regions past every chunk's, and the merge copies them back
     uint64_t nl_tot = 0;
+    for (int32_t k = 0; k < n; k++)
+        nl_tot = std::max<uint64_t>(nl_tot, sh->h_jobs[(size_t)k].nl_off + sh->h_jobs[(size_t)k].nl_cap);
     int32_t t = 0;
     for (int32_t k = 0; k < n; k++) {
         const PpgInflateJob &C = sh->h_jobs[(size_t)k];
         const int64_t from_out = PO[(size_t)k];
+        if (hidx[(size_t)k + 1] - hidx[(size_t)k] == 1) {
+            sh->h_sjobs[hidx[(size_t)k]] = C;
+            continue;
+        }
         for (uint32_t j = hidx[(size_t)k]; j < hidx[(size_t)k + 1]; j++) {
             PpgInflateJob J = C;
             int64_t lo = 0;   // chunk-relative start of this piece
@@ -736,7 +743,9 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     HIPCHK(sh->sres.alloc(sh->h_sjobs.size()));
     HIPCHK(sh->sidx.alloc(hidx.size()));
     HIPCHK(hipMemcpyAsync(sh->sidx.p, hidx.data(), 4 * hidx.size(), hipMemcpyHostToDevice, s));
-    HIPCHK(sh->snls.alloc((size_t)nl_tot + 64));
+    if ((size_t)nl_tot + 64 > sh->nls.n) {   // grow, keeping nothing (the next run rewrites it)
+        HIPCHK(sh->nls.alloc((size_t)nl_tot + 64));
+    }
     HIPCHK(hipStreamSynchronize(s));   // staging vectors and d2 (the old dictionaries) die here
     sh->nsub = nsub;
     return PPG_OK;

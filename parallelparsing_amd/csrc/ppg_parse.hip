@@ -257,8 +257,9 @@ extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
 // start at deflate block boundaries inside it, each with its own 32 KiB history.  Their results
 // are folded into the chunk's (in order: the first failing sub-job's status; every sub-job but
 // the last must produce exactly its bytes and end exactly where the next one starts), and their
-// stored newline positions -- already chunk-relative raw indices -- are concatenated into the
-// chunk's own census region, so the parse kernels see the chunk as one job.  One block per chunk.
+// stored newline positions -- already chunk-relative raw indices, in regions of the same buffer
+// past every chunk's own -- are concatenated into the chunk's region, so the parse kernels see the
+// chunk as one job.  A chunk decoded whole censused straight into its region.  One block per chunk.
 // ------------------------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(256) void ppg_split_merge(const PpgInflateJob *__restrict__ sjobs,
                                                                   const PpgInflateResult *__restrict__ sres,
@@ -270,6 +271,10 @@ extern "C" __global__ __launch_bounds__(256) void ppg_split_merge(const PpgInfla
     const int k = blockIdx.x;
     if (k >= n) return;
     const uint32_t s0 = sidx[k], s1 = sidx[k + 1];
+    if (s1 == s0 + 1) {   // decoded whole: its census is already in the chunk's region
+        if (threadIdx.x == 0) res[k] = sres[s0];
+        return;
+    }
     const PpgInflateJob &C = jobs[k];
     PpgInflateResult m = {};
     uint32_t nl = 0;
