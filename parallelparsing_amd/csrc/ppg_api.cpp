@@ -904,6 +904,17 @@ static void ingest_free(IngestState *st) {
 
 extern "C" {
 
+// the index's side points inside chunks [first, first+n) -> ppg_shard_set_split (host ingest)
+static int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n) {
+    const int64_t lo = ix->pts[(size_t)first].output, hi = ix->pts[(size_t)first + n].output;
+    const auto &O = ix->side_out;
+    const size_t a = (size_t)(std::upper_bound(O.begin(), O.end(), lo) - O.begin());
+    const size_t b = (size_t)(std::lower_bound(O.begin(), O.end(), hi) - O.begin());
+    if (b <= a) return PPG_OK;
+    return ppg_shard_set_split(sh, (int32_t)(b - a), ix->side_bit.data() + a, O.data() + a,
+                               ix->side_win.data() + a * kWin);
+}
+
 int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
                             int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,
                             double *seconds) {
@@ -919,6 +930,15 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
     const int fd = open(gz_path, O_RDONLY);
     if (fd < 0) return PPG_IO_ERROR;
     struct FdClose { int fd; ~FdClose() { close(fd); } } fdc{fd};
+
+    // an index with side points (ppg_index_build_gpu_side) splits chunks when the file has too few
+    // of them to fill the GPU a few times over (the ~6 generations bench.py's auto split uses)
+    bool split = false;
+    if (!ix->side_out.empty()) {
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        split = (int64_t)n < 6 * 32 * (int64_t)cus;
+    }
 
     // pieces: consecutive chunks of about piece_bytes compressed bytes (at least one chunk).
     // (Ramping the first / last pieces down measured slower: one chunk alone takes ~100 ms, so
@@ -993,6 +1013,9 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             if (rcp == PPG_OK)
                 rcp = shard_prepare(S.sh[k % kPieces], ix, first + pieces[k].first, pieces[k].second - pieces[k].first, dst,
                                     len, 0, S.cs);
+            if (rcp == PPG_OK && split)
+                rcp = shard_split_from_index(S.sh[k % kPieces], ix, first + pieces[k].first,
+                                             pieces[k].second - pieces[k].first);
             if (verbose)
                 fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms, prepare %.1f ms\n", k,
                         len / 1e6, t1, t2 - t1, now_ms() - t2);

@@ -233,3 +233,20 @@ def test_side_points_split_decompress_all(side, cap, pigz, device):
     _, j1, _, _ = ix.point_fields(5)
     s3 = pp.Shard(ix, gz[j0 - 1:j1], 2, 3, device=device).set_split(b2, o2, w2).run()
     assert (s3.results()["records"] == ra["records"][2:5]).all()
+
+
+@pytest.mark.parametrize("piece", [4 << 20, 8 << 30])
+def test_file_ingest_uses_side_points(piece, tmp_path, device):
+    """Host ingest (ppg_file_decompress_all) with an index that carries side points splits the
+    chunks of a small file (too few to fill the GPU): the same per-chunk records as without."""
+    nrec = 120_000
+    gz = synth_gz(fastq_text(nrec, seed=33), level=6, piece=4 << 20)
+    p = tmp_path / "s.gz"
+    p.write_bytes(gz)
+    plain = pp.Core.BuildDeflateIndexGpu(gz, 10000, device=device)
+    side = pp.Core.BuildDeflateIndexGpu(gz, 10000, device=device, side_bytes=200_000)
+    assert side.side_points()[0].size > side.Count
+    r0, t0, _ = pp.decompress_file(plain, str(p), piece_bytes=piece, threads=4, device=device)
+    r1, t1, _ = pp.decompress_file(side, str(p), piece_bytes=piece, threads=4, device=device)
+    assert t0 == t1 == nrec
+    assert (r0 == r1).all()
