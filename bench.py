@@ -255,7 +255,8 @@ def paired_run(args, dev):
 def auto_split(args, dev, chunks):
     """(S, K): split the last K of a rank's chunks into up to S waves each (ppg_shard_set_split).
     --split S > 0: every chunk.  --split 0 (auto): a rank holding fewer than ~6 generations of
-    resident waves (CUs x 32) splits every chunk, into enough waves for ~6 generations (at most 16);
+    resident waves (CUs x 32) splits every chunk, into enough waves for ~6 generations (at most 64:
+    in practice every inner block start, ~15 per 10k-record chunk);
     a larger rank splits only its last generation, into 4, so the launch's tail drains in a
     quarter of a chunk's time.  Measured on one MI355X."""
     if args.split > 0:
@@ -263,7 +264,7 @@ def auto_split(args, dev, chunks):
     import torch
     slots = torch.cuda.get_device_properties(dev).multi_processor_count * 32
     if chunks < 6 * slots:
-        return int(min(16, max(1, -(-6 * slots // max(1, chunks))))), chunks
+        return int(min(64, max(1, -(-6 * slots // max(1, chunks))))), chunks
     return args.tail_split, min(chunks, int(args.tail_gens * slots))
 
 
