@@ -308,11 +308,20 @@ def main():
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     import torch
+    # rehearsal knobs (never set by the driver): PPG_BENCH_ONE_DEVICE=1 puts every rank on cuda:0 and
+    # PPG_DIST_BACKEND=gloo exchanges through host memory, so the N > 1 path runs on a 1-GPU box
+    if os.environ.get("PPG_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("PPG_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+        else:
+            dist.init_process_group(backend)
+    xdev = dev if backend == "nccl" else torch.device("cpu")   # where collectives' tensors live
 
     import parallelparsing_amd as pp
     from parallelparsing_amd.dist import partition_chunks, gather_counts
@@ -353,7 +362,7 @@ def main():
         shard.run()
         if world > 1:
             shard.counts_to_device(counts_dev.data_ptr())
-            return gather_counts(counts_dev[: b - a], ranges, device=dev)
+            return gather_counts(counts_dev[: b - a].to(xdev), ranges, device=xdev)
         return None
 
     for _ in range(args.warmup):
@@ -373,7 +382,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
