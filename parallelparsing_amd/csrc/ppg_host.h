@@ -61,10 +61,8 @@ struct ppg_index {
         p.input = input;
         p.bits = bits;
         // oldest bytes (those after the circular write head) first
-        const size_t w0 = windows.size();
-        windows.resize(w0 + kWin);
-        std::copy(circ + (kWin - left), circ + kWin, windows.begin() + w0);
-        std::copy(circ, circ + (kWin - left), windows.begin() + w0 + left);
+        windows.insert(windows.end(), circ + (kWin - left), circ + kWin);
+        windows.insert(windows.end(), circ, circ + (kWin - left));
         p.offset.assign(off, off + off_len);
         pts.push_back(std::move(p));
     }

@@ -516,19 +516,28 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             if (p.output > 0) gw.push_back(PpgGather{h2[p.j].out_off, (uint64_t)p.j * kWin, p.rel, ~0ull, 0});
         const size_t npick_w = gw.size();
         for (const Side &d : sides) gw.push_back(PpgGather{h2[d.j].out_off, (uint64_t)d.j * kWin, d.rel, ~0ull, 0});
-        std::vector<uint8_t> hw(gw.size() * kWin);
+        // host staging of the gathered windows: uninitialised (a zero-filled vector of ~1.7 GB per
+        // 50 GB member costs a memset), and the index's window array grows once per batch
+        const size_t hw_n = gw.size() * kWin;
+        std::unique_ptr<uint8_t[]> hw_buf(new uint8_t[std::max<size_t>(hw_n, 1)]);
+        uint8_t *const hw = hw_buf.get();
+        ix.pts.reserve(ix.pts.size() + picks.size());
+        ix.windows.reserve(ix.windows.size() + picks.size() * kWin);
+        ix.side_bit.reserve(ix.side_bit.size() + sides.size());
+        ix.side_out.reserve(ix.side_out.size() + sides.size());
+        ix.side_win.reserve(ix.side_win.size() + sides.size() * kWin);
         if (!gw.empty()) {
             HIPCHK(B.gat.alloc(gw.size()));
             HIPCHK(dwin.alloc(gw.size() * kWin));
             HIPCHK(hipMemcpyAsync(B.gat.p, gw.data(), sizeof(PpgGather) * gw.size(), hipMemcpyHostToDevice, s));
             HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, dwin.p, nullptr, nullptr, (int)gw.size()));
-            HIPCHK(hipMemcpyAsync(hw.data(), dwin.p, hw.size(), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(hw, dwin.p, hw_n, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
         for (size_t i = 0; i < sides.size(); i++) {
             ix.side_bit.push_back((int64_t)sides[i].end_bit);
             ix.side_out.push_back(sides[i].output);
-            const uint8_t *w = hw.data() + (npick_w + i) * kWin;
+            const uint8_t *w = hw + (npick_w + i) * kWin;
             ix.side_win.insert(ix.side_win.end(), w, w + kWin);
         }
         size_t wi = 0;
@@ -536,7 +545,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             if (p.output == 0) {
                 ix.add_point((int)p.bits, p.input, 0, 0, zeros.data(), nullptr, 0);
             } else {
-                const uint8_t *w = hw.data() + (wi++) * kWin;
+                const uint8_t *w = hw + (wi++) * kWin;
                 ix.add_point((int)p.bits, p.input, p.output, 0, w, w + kWin - p.off_len, (size_t)p.off_len);
             }
         }
