@@ -195,7 +195,7 @@ def paired_run(args, dev):
     # one ctx (= one HIP stream) per file, so the two DecompressAll passes run concurrently: at
     # chunk = 50,000 one file has only ~2.7k chunks, a third of the GPU's 8k wave slots
     ctxs = [pp.Device(dev.index), pp.Device(dev.index)]
-    args.split, _ = auto_split(args, dev, sum(tf.npoints - 1 for tf in tfs))
+    args.split, _ = auto_split(args, wave_slots(dev), sum(tf.npoints - 1 for tf in tfs))
     shards, bufs = [], []
     for tf, ctx in zip(tfs, ctxs):
         lo, hi = int(tf.p_input[0]) - 1, int(tf.p_input[-1])
@@ -252,7 +252,13 @@ def paired_run(args, dev):
     }
 
 
-def auto_split(args, dev, chunks):
+def wave_slots(dev):
+    """Resident wave slots of the GPU: CUs x 32 (8 waves per SIMD, the inflate kernel's occupancy)."""
+    import torch
+    return torch.cuda.get_device_properties(dev).multi_processor_count * 32
+
+
+def auto_split(args, slots, chunks):
     """(S, K): split the last K of a rank's chunks into up to S waves each (ppg_shard_set_split).
     --split S > 0: every chunk.  --split 0 (auto): a rank holding fewer than ~6 generations of
     resident waves (CUs x 32) splits every chunk, into enough waves for ~6 generations (at most 64:
@@ -261,8 +267,6 @@ def auto_split(args, dev, chunks):
     quarter of a chunk's time.  Measured on one MI355X."""
     if args.split > 0:
         return args.split, chunks
-    import torch
-    slots = torch.cuda.get_device_properties(dev).multi_processor_count * 32
     if chunks < 6 * slots:
         return int(min(64, max(1, -(-6 * slots // max(1, chunks))))), chunks
     return args.tail_split, min(chunks, int(args.tail_gens * slots))
@@ -348,7 +352,7 @@ def main():
     out_cap = int(args.out_capacity_gib * (1 << 30))
     shard = pp.Shard(index, comp.data_ptr(), first=0, n=b - a, device=ctx, comp_on_device=True, comp_len=comp_len,
                      out_capacity=out_cap)
-    args.split, ksplit = auto_split(args, dev, b - a)
+    args.split, ksplit = auto_split(args, wave_slots(dev), b - a)
     if args.split > 1:
         sb, so, sw = tf.side_points(b - ksplit, b + 1, args.split)
         shard.set_split(sb, so, sw)

@@ -1,0 +1,35 @@
+"""bench.py's choice of split chunks (ppg_shard_set_split), host logic only: MI355X = 256 CUs x 32
+resident waves.  Measured basis: DESIGN.md §5 and §7."""
+import argparse
+
+import pytest
+
+import bench
+
+SLOTS = 256 * 32
+
+
+def args(split=0, tail_split=8, tail_gens=0.5):
+    return argparse.Namespace(split=split, tail_split=tail_split, tail_gens=tail_gens)
+
+
+@pytest.mark.parametrize("chunks,expect", [
+    (52735, (8, 4096)),      # the default 50 GB step: only the last half-generation, into <= 8
+    (26498, (2, 26498)),     # strong-scaling rank share at N = 2
+    (13249, (4, 13249)),     # N = 4
+    (6755, (8, 6755)),       # N = 8
+    (97, (64, 97)),          # the 1 M-read file: every inner block start
+    (1, (64, 1)),
+])
+def test_auto_split(chunks, expect):
+    assert bench.auto_split(args(), SLOTS, chunks) == expect
+
+
+def test_explicit_split_covers_every_chunk():
+    assert bench.auto_split(args(split=3), SLOTS, 52735) == (3, 52735)
+    assert bench.auto_split(args(split=1), SLOTS, 97) == (1, 97)
+
+
+def test_tail_knobs():
+    assert bench.auto_split(args(tail_split=1), SLOTS, 60000) == (1, 4096)   # off: S = 1
+    assert bench.auto_split(args(tail_gens=2.0), SLOTS, 60000) == (8, 16384)

@@ -145,3 +145,9 @@ def test_record_keys_drop_q1_duplicates(tmp_path):
     assert sh.total_records > nrec                       # the reference's duplicates are there
     assert int((keys == paired.DUP).sum()) == sh.total_records - nrec
     assert torch.equal(kept.cpu(), torch.arange(1, nrec + 1))
+    # the same keys with every chunk split at its inner block start (bench --paired's auto split)
+    from test_gpu_parity import dense_side_points
+    bits, outs, win = dense_side_points(gz, ix)
+    assert bits.size >= n // 2
+    s2 = pp.Shard(ix, np.frombuffer(gz[i0 - 1:i1], np.uint8), 0, n).set_split(bits, outs, win).run()
+    assert torch.equal(paired.shard_keys(s2), keys)
