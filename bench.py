@@ -358,6 +358,7 @@ def main():
         shard.set_split(sb, so, sw)
         log(f"[bench] rank {rank}: last {ksplit} chunks split, {b - a + sb.size} waves ({sb.size} side points)")
     args.split_chunks = ksplit if args.split > 1 else 0
+    n_side = int(sb.size) if args.split > 1 else 0
     log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
         f"{shard.batches} output batch(es), setup {time.time() - t:.1f}s")
     counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
@@ -437,7 +438,14 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload, shard.batches),
                      "kernel": "ppg_inflate_kernel", "alg_bytes_per_launch": alg_local / shard.batches,
-                     "mean_launch_ms": mean_launch_s * 1e3},
+                     "mean_launch_ms": mean_launch_s * 1e3,
+                     # SURVEY §8d's secondary terms (not in alg_bytes), per launch of this rank
+                     "secondary_bytes_per_launch": {
+                         "windows": 32768 * (b - a + n_side) // shard.batches,
+                         "offsets": int(tf.p_offlen[a:b].sum()) // shard.batches,
+                         "census_positions": 2 * 4 * 4 * local_records // shard.batches,   # 4 B per newline, written + read
+                         "descriptors": 16 * local_records // shard.batches,
+                         "parse_reread": 0}},   # the newline census is fused into the inflate flush
         "reference_published_rec_s": REFERENCE_REC_S,
     }
     if rank == 0 and world == 1 and (args.ingest or args.create_index):
