@@ -301,6 +301,9 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, con
 // in flight).  Written out because the compiler turns the emit's far-byte load into exec-mask
 // juggling (~9 SALU per round) or a 64-bit per-lane address.  The wait also covers the stream's
 // LDS-DMA issued before it, as any vmcnt wait here did.
+// No wait states precede the load: the base pair must not be written by a VALU (a spill restore)
+// just before it -- tools/hazard_lint.py checks the compiled kernel for that at every build (with
+// amdgpu_num_sgpr(64) the base was spilled and the load faulted; padding costs 0.6%).
 __device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) {
     uint32_t v;
     asm volatile("global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
