@@ -67,3 +67,15 @@ def test_side_points_are_block_starts(records, repeats, chunk, per):
     for k in range(o.size - 1):
         assert O.extract(f, ix, k) == text[o[k]:o[k + 1]], k
         assert w[k].tobytes() == (b"\0" * 32768 + text[:o[k]])[-32768:], k
+
+
+def test_side_points_of_a_range_match_the_whole():
+    """bench.py splits only a rank's last chunks: side_points(lo, hi) equals the whole member's
+    side points that fall inside chunks lo..hi-2 (the rule is per chunk)."""
+    tf = TiledFile(3000, 5, 700, threads=4)
+    b_all, o_all, w_all = tf.side_points(per_chunk=4)
+    lo, hi = 3, tf.npoints - 2
+    b, o, w = tf.side_points(lo, hi, per_chunk=4)
+    keep = (o_all > tf.p_output[lo]) & (o_all < tf.p_output[hi - 1])
+    assert np.array_equal(o, o_all[keep]) and np.array_equal(b, b_all[keep])
+    assert w.tobytes() == w_all.reshape(-1, 32768)[keep].tobytes()
