@@ -27,7 +27,12 @@ def shard_keys(shard):
     (int64; DUP / NOKEY markers kept).  GPU kernel ppg_record_keys."""
     import torch
     n = shard.total_records
-    keys = torch.empty(max(n, 1), dtype=torch.int64, device=torch.device("cuda", shard.dev.device))
+    dev = torch.device("cuda", shard.dev.device)
+    keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    # the kernel writes on the shard's own stream: torch's caching allocator may have handed out a
+    # block that kernels still queued on torch's stream read (e.g. a boolean mask freed by the caller
+    # while its gather is in flight), so let torch's stream drain first
+    torch.cuda.current_stream(dev).synchronize()
     check(lib.ppg_shard_keys(shard.handle, C.c_void_p(keys.data_ptr()), n), "ppg_shard_keys")
     return keys[:n]
 
