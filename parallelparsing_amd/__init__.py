@@ -272,6 +272,8 @@ class Core:
                 raise ValueError("side_bytes needs the member in memory (host or device)")
             rc = lib.ppg_index_build_gpu_file(dev.handle, os.fsencode(gz), cs, int(piece_bytes), C.byref(h))
         elif hasattr(gz, "data_ptr"):
+            import torch
+            torch.cuda.current_stream(gz.device).synchronize()   # our stream reads what torch's wrote
             rc = lib.ppg_index_build_gpu_side(dev.handle, C.c_void_p(gz.data_ptr()), gz.numel(), 1, cs,
                                               int(piece_bytes), int(out_capacity), int(side_bytes), C.byref(h))
         else:
