@@ -215,6 +215,46 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_place(
 // first record of a chunk that lies wholly inside offset_k is the previous chunk's last record
 // parsed again (the Point fell on a record start) and gets -2, so a pairing can drop
 // it and keep global record numbers aligned.  One block per chunk, a thread per record.
+// The spot number of an identifier whose bytes start at p (L of them before the line's end or
+// the 96-byte bound): the digits between the first two '.', 1..18 of them, else -1 -- the byte
+// loop of ppg_record_keys, over 48 bytes gathered as 13 aligned dwords (one load each instead of
+// one dependent byte load per character).  Returns 1 when the window ends before the answer does.
+// p + 52 stays inside the output buffer (a 64-byte tail follows it).
+__device__ __forceinline__ int spot_key_window(const uint8_t *p, uint64_t L_total, int64_t &key) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t x[13], u[12];
+#pragma unroll
+    for (int k = 0; k < 13; k++) x[k] = w[k];
+#pragma unroll
+    for (int k = 0; k < 12; k++) u[k] = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+    const uint32_t L = (uint32_t)min(L_total, (uint64_t)48);
+    int state = 0;   // 0: before the first '.', 1: digits, 2: done
+    int64_t v = 0;
+    int nd = 0;
+    key = -1;
+#pragma unroll
+    for (int i = 0; i < 48; i++) {
+        const uint32_t c = (u[i >> 2] >> (8 * (i & 3))) & 255u;
+        const bool in = (uint32_t)i < L;
+        if (state == 0) {
+            if (!in) state = 2;                       // the line ended: -1
+            else if (c == '.') state = 1;
+        } else if (state == 1) {
+            if (!in) state = 2;                       // the line ended inside the digits: -1
+            else if (c >= '0' && c <= '9') {
+                if (nd == 18) state = 2;              // a 19th digit: -1
+                else { v = v * 10 + (int64_t)(c - '0'); nd++; }
+            } else {
+                if (c == '.' && nd > 0) key = v;
+                state = 2;
+            }
+        }
+    }
+    return state == 2 || L_total <= 48 ? 0 : 1;
+}
+
 extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
     const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
     const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, const PpgParseInfo *__restrict__ info,
@@ -235,6 +275,11 @@ extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
         int64_t key = -1;
         uint64_t i = start + 1;
         const uint64_t end = min(n1, start + 96);   // identifiers are short; bound the scan
+        if (start >= olen) {   // the identifier lies in the body: its first 48 bytes in registers
+            const int r2 = spot_key_window(body + (start + 1 - olen), end > start + 1 ? end - start - 1 : 0, key);
+            if (r2 == 0) { kk[j] = key; continue; }
+            key = -1;           // not settled inside the window: the byte loop below
+        }
         while (i < end && raw_at(off, olen, body, blen, i) != '.') i++;
         if (i < end) {
             i++;
