@@ -12,11 +12,17 @@ N > 1.  Decompressed output streams through a reused device buffer (out_capacity
 consumer enumerating records would.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 50gb|1m]
-  (N > 1: launched by torch.distributed.run, one process per GPU, backend nccl = RCCL)
+  N > 1: one process per GPU, backend nccl = RCCL.  Under torch.distributed.run (WORLD_SIZE set)
+  this process is one rank; started directly with --gpus N > 1 it launches the N ranks itself
+  (torch.distributed.run as a child, before anything touches the GPU) and exits with its code.
+  N > 1 defaults to strong scaling: one ~50 GB member split over the N GPUs (configs[3]).
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -49,9 +55,40 @@ def build_input(args):
     return tf
 
 
+def host_cpu_info():
+    """What the CPU baseline ran on: nproc, the scheduler affinity, the cgroup quota, the model."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            info["model"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        info["model"] = None
+    return info
+
+
+def _timed(fn, warm, runs):
+    """BASELINE.md §2 protocol: `warm` untimed runs, then the median of `runs` timed ones."""
+    for _ in range(warm):
+        fn()
+    ts, res = [], None
+    for _ in range(runs):
+        t = time.perf_counter()
+        res = fn()
+        ts.append(time.perf_counter() - t)
+    return res, statistics.median(ts), ts
+
+
 def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
     """The oracle's threaded DecompressAll (C restatement of BatchedFASTQ over zlib 1.2.11) on a
-    bounded prefix of the same file, timed on this host (rank 0, N = 1 only)."""
+    bounded prefix of the same file, timed on this host (rank 0, N = 1 only): T = every host core
+    (os.cpu_count()), 2 warm-ups + the median of 5, plus one thread and the
+    C#-shaped consumer that materialises every record as FastqRecord does (median of 3 each)."""
     from oracle import oracle as O
     sample = min(nchunks, int(os.environ.get("PPG_CPU_SAMPLE_CHUNKS", "4096")))
     hi = int(ix_in[sample])
@@ -59,23 +96,20 @@ def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
     win, offs = tf.windows(0, sample + 1)
     oi = O.index_from_points(tf.p_output[: sample + 1], tf.p_input[: sample + 1], tf.p_bits[: sample + 1],
                              win, tf.p_offlen[: sample + 1], offs)
-    O.decompress_all(gz, oi, threads=threads, first=0, last=min(sample, 16))   # warm
-    t = time.perf_counter()
-    recs, _ = O.decompress_all(gz, oi, threads=threads, first=0, last=sample)
-    dt = time.perf_counter() - t
+    (recs, _), dt, ts = _timed(lambda: O.decompress_all(gz, oi, threads=threads, first=0, last=sample), 2, 5)
     out_bytes = int(ix_out[sample] - ix_out[0])
     # SURVEY 8d variants: one thread, and the C#-shaped consumer that materialises every record
     # into its own buffer as FastqRecord does (Parsing.cs:41-47, mode 1), on smaller prefixes
     variants = {}
-    for name, th, mode, n in (("1 thread", 1, 0, min(sample, 256)),
+    for name, th, mode, n in (("1 thread", 1, 0, min(sample, 128)),
                               (f"{threads} threads, records materialised", threads, 1, min(sample, 2048))):
-        t1 = time.perf_counter()
-        r1, _ = O.decompress_all(gz, oi, threads=th, mode=mode, first=0, last=n)
-        d1 = time.perf_counter() - t1
-        variants[name] = {"records_per_s": r1 / d1, "cores": th, "chunks": n, "seconds": d1}
+        (r1, _), d1, _ = _timed(lambda: O.decompress_all(gz, oi, threads=th, mode=mode, first=0, last=n), 1, 3)
+        variants[name] = {"records_per_s": r1 / d1, "cores": th, "chunks": n, "seconds_median": d1}
     return {"value": recs / dt, "unit": "records/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} of {nchunks} chunks ({recs:,} records, {out_bytes / 1e9:.2f} GB out) "
-                      f"of the same file, {threads} threads, {dt:.2f} s",
+                      f"of the same file, {threads} threads (= os.cpu_count()), median of 5 after 2 warm-ups: "
+                      f"{dt:.2f} s",
+            "runs_s": [round(t, 3) for t in ts], "host": host_cpu_info(),
             "decompressed_MBps": out_bytes / dt / 1e6, "variants": variants}
 
 
@@ -272,6 +306,41 @@ def auto_split(args, slots, chunks):
     return args.tail_split, min(chunks, int(args.tail_gens * slots))
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_cmd(n, argv, port):
+    """The torch.distributed.run command that starts n ranks of this script on one node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` without a launcher: start the N ranks (one process per GPU) as a
+    child torch.distributed.run and return its exit code.  Nothing in this process has touched the
+    GPU, and it starts a child rather than exec-ing (rank 0's JSON line passes straight through)."""
+    cmd = launch_cmd(n, argv, _free_port())
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd).returncode
+
+
+def rccl_info(world, backend):
+    """The communicator the run actually used (reported in the line)."""
+    import torch
+    import torch.distributed as dist
+    info = {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None}
+    try:
+        info["rccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
+    except Exception:   # noqa: BLE001 - informational only
+        info["rccl_version"] = None
+    return info
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -281,8 +350,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=10000)
     ap.add_argument("--seg-records", type=int, default=2_621_440)   # ~1 GB of text per segment
     ap.add_argument("--repeats", type=int, default=203)             # per GPU: ~50 GB gz, ~532 M records
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: ~50 GB of gzip per GPU (default); strong: one ~50 GB member over N GPUs")
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="strong (default for N > 1, BASELINE configs[3]): one ~50 GB member split over the N "
+                         "GPUs; weak: ~50 GB of gzip per GPU")
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -300,17 +370,27 @@ def main():
                          "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
                          "0 (default) = auto: enough waves for ~6 generations of the GPU's wave slots (S = 1 for "
                          "the default 50 GB-per-GPU workload, 8 for a strong-scaled rank at N = 8)")
-    ap.add_argument("--ingest", action="store_true",
-                    help="also time DecompressAll straight from the .gz file on disk (host ingest, PCIe-inclusive; "
-                         "reported under 'ingest', never as value)")
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="skip the end-to-end leg (N = 1): DecompressAll straight from the .gz file on disk (host "
+                         "ingest, PCIe-inclusive; reported under 'ingest', never as value)")
+    ap.add_argument("--ingest", action="store_true", help=argparse.SUPPRESS)   # on by default since r02
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     args.world = world
+    if args.scaling is None:
+        args.scaling = "strong" if world > 1 else "weak"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if os.environ.get("PPG_BENCH_DRYRUN"):   # launcher test (tests/test_bench_launch.py): no GPU
+        with open(os.path.join(os.environ["PPG_BENCH_DRYRUN"], f"rank{rank}.json"), "w") as f:
+            json.dump({"rank": rank, "local_rank": local, "world": world, "scaling": args.scaling,
+                       "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}, f)
+        return
     import torch
     # rehearsal knobs (never set by the driver): PPG_BENCH_ONE_DEVICE=1 puts every rank on cuda:0 and
     # PPG_DIST_BACKEND=gloo exchanges through host memory, so the N > 1 path runs on a 1-GPU box
@@ -447,16 +527,21 @@ def main():
                          "descriptors": 16 * local_records // shard.batches,
                          "parse_reread": 0}},   # the newline census is fused into the inflate flush
         "reference_published_rec_s": REFERENCE_REC_S,
+        "communicator": rccl_info(world, backend),
     }
+    args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest
     if rank == 0 and world == 1 and (args.ingest or args.create_index):
         del shard, comp
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and args.create_index:
         line["create_index"] = create_index_run(tf, args, dev)
     if rank == 0 and world == 1 and args.ingest:
-        line["ingest"] = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads)
+        try:
+            line["ingest"] = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads)
+        except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
+            line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        threads = min(512, os.cpu_count() or 1)   # every host core (capped for the pid limit)
         line["cpu_baseline"] = cpu_baseline(tf, ix_out, ix_in, nchunks, threads)
     if rank == 0:
         print(json.dumps(line), flush=True)

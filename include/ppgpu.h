@@ -100,12 +100,33 @@ const uint8_t *ppg_index_window(const ppg_index *ix, int32_t i);  /* Point.Windo
 const uint8_t *ppg_index_offset(const ppg_index *ix, int32_t i);  /* Point.offset */
 void ppg_index_free(ppg_index *ix);
 
+/* Whether chunks [first, first+n) fit the decode kernels (checked by ppg_shard_create and every
+ * decode entry point): PPG_OK; PPG_UNSUPPORTED for a chunk whose output (+ its offset carry) is
+ * 2^31 bytes or more -- where the reference's (int)(to.Output - from.Output) (Core.cs:140) already
+ * breaks -- or whose compressed span is 2^32 - 2^12 bits or more; PPG_ARG_ERROR for Points out of
+ * order or a range outside the index.  Host-only; needs no device. */
+int ppg_index_validate(const ppg_index *ix, int32_t first, int32_t n);
+
 /* ================================= device context ================================= */
 
 int ppg_device_count(int *n);
 int ppg_open(int device, ppg_ctx **out);
 void ppg_close(ppg_ctx *ctx);
 void *ppg_ctx_stream(ppg_ctx *ctx); /* the hipStream_t every kernel of this ctx runs on */
+
+/* Stream-ordered handoff between the ctx's stream and a caller's hipStream_t (torch's current
+ * stream, a host's own), with no host synchronisation -- the device-side counterpart of the
+ * reference's per-call ZStream ownership (Interop/Conventions.cs:43-127):
+ *   ppg_ctx_wait_stream: work queued on the ctx from now on waits for everything already queued on
+ *     `stream` (call it before a ppg call reads device memory that `stream` writes, or writes
+ *     memory that `stream` may still read, e.g. a block a caching allocator recycled);
+ *   ppg_stream_wait_ctx: work queued on `stream` from now on waits for everything already queued
+ *     on the ctx.
+ * Every ppg entry point that reads caller device memory (comp_on_device, gz_on_device) or writes it
+ * (ppg_shard_keys, ppg_shard_counts_to_device, ppg_shard_copy_output) does so on the ctx's
+ * stream, so one ppg_ctx_wait_stream before the call orders it after the caller's producers. */
+int ppg_ctx_wait_stream(ppg_ctx *ctx, void *stream);
+int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream);
 
 /* ====================== Decompress one checkpoint (README "Decompress") ======================
  * Core.ExtractDeflateIndex(fileBuffer, from=Index[k], to=Index[k+1], buf) — Core.cs:133-192,
@@ -161,6 +182,10 @@ int32_t ppg_shard_batches(ppg_shard *sh);
 int ppg_shard_copy_chunk(ppg_shard *sh, int32_t k, uint8_t *dst, int64_t cap, int64_t *len);
 int ppg_shard_copy_records(ppg_shard *sh, int32_t k, uint32_t *dst, int64_t cap, int64_t *nrec);
 int ppg_shard_record_base(ppg_shard *sh, int64_t *base); /* n record bases (exclusive scan) */
+/* Bytes [off, off+len) of a one-batch shard's decompressed output (off relative to
+ * Index[first].Output; chunks are contiguous) into host memory or (dst_on_device) device memory
+ * on this GPU, on the ctx stream. */
+int ppg_shard_copy_output(ppg_shard *sh, int64_t off, int64_t len, void *dst, int dst_on_device);
 
 /* Paired reads (the reference only names the goal, README.md:9): the spot number
  * of every record of a one-batch shard, in record order, into caller device memory (cap int64s):

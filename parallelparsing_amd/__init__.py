@@ -80,6 +80,14 @@ class Index:
         off = C.string_at(lib.ppg_index_offset(self._h, i), ol) if ol else b""
         return Point(o, n, b, w, off)
 
+    def validate(self, first=0, n=None):
+        """ppg_index_validate: raises PpgError(PPG_UNSUPPORTED) if a chunk of [first, first+n) is
+        too large for the decode kernels (output >= 2^31 bytes, or >= 2^32 - 2^12 compressed bits)."""
+        if n is None:
+            n = self.Count - 1 - first
+        check(lib.ppg_index_validate(self._h, int(first), int(n)), "Index.validate")
+        return self
+
     def arrays(self):
         """(output, input, bits) int64 numpy arrays over all points."""
         n = self.Count
@@ -165,6 +173,21 @@ class Device:
     def stream(self):
         return lib.ppg_ctx_stream(self._h)
 
+    def wait_stream(self, stream):
+        """Order this ctx's later work after everything queued on `stream` (a hipStream_t handle, or
+        a torch.cuda.Stream) so far -- ppg_ctx_wait_stream, no host drain."""
+        check(lib.ppg_ctx_wait_stream(self._h, C.c_void_p(_stream_handle(stream))), "ppg_ctx_wait_stream")
+
+    def stream_wait(self, stream):
+        """Order `stream`'s later work after everything queued on this ctx so far (ppg_stream_wait_ctx)."""
+        check(lib.ppg_stream_wait_ctx(self._h, C.c_void_p(_stream_handle(stream))), "ppg_stream_wait_ctx")
+
+    def after_torch(self):
+        """wait_stream(torch's current stream on this device): call before a ppg call reads device
+        memory torch's stream writes, or writes memory it may still read."""
+        import torch
+        self.wait_stream(torch.cuda.current_stream(torch.device("cuda", self.device)))
+
     @classmethod
     def default(cls, device=None):
         if device is None:
@@ -172,6 +195,12 @@ class Device:
         if device not in cls._default:
             cls._default[device] = cls(device)
         return cls._default[device]
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return 0
+    return int(getattr(stream, "cuda_stream", stream))
 
 
 def device_count():
@@ -273,7 +302,14 @@ class Core:
             rc = lib.ppg_index_build_gpu_file(dev.handle, os.fsencode(gz), cs, int(piece_bytes), C.byref(h))
         elif hasattr(gz, "data_ptr"):
             import torch
-            torch.cuda.current_stream(gz.device).synchronize()   # our stream reads what torch's wrote
+            if not (gz.is_cuda and gz.dtype == torch.uint8 and gz.is_contiguous() and gz.dim() == 1):
+                raise ValueError("BuildDeflateIndexGpu: a device tensor must be a contiguous 1-D uint8 CUDA tensor")
+            if gz.data_ptr() % 4:
+                raise ValueError("BuildDeflateIndexGpu: a device tensor must be 4-byte aligned")
+            # the block finder and the inflate reader fetch whole 4-byte words and read ahead: bytes
+            # past gz_len may be read (never used), so they must be mapped -- torch's caching
+            # allocator rounds every block up to 512 B; ppgpu.h documents the requirement
+            dev.wait_stream(torch.cuda.current_stream(gz.device))   # our stream reads what torch's wrote
             rc = lib.ppg_index_build_gpu_side(dev.handle, C.c_void_p(gz.data_ptr()), gz.numel(), 1, cs,
                                               int(piece_bytes), int(out_capacity), int(side_bytes), C.byref(h))
         else:
@@ -328,8 +364,12 @@ class Shard:
         if n is None:
             n = index.Count - 1 - first
         self.first, self.n = first, n
+        self._on_device = bool(comp_on_device)
         if comp_on_device:
             ptr, length = int(comp), int(comp_len)
+            # the library reads comp on its own stream: order that after torch's producers of comp
+            # (a caller on another stream calls self.dev.wait_stream(its stream) itself)
+            self._torch_order()
         else:
             self._host = _as_u8(comp)
             ptr, length = self._host.ctypes.data, self._host.size
@@ -348,9 +388,34 @@ class Shard:
     def handle(self):
         return self._h
 
+    def _torch_order(self):
+        import sys
+        if "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized():
+            self.dev.after_torch()
+
     def run(self):
+        if self._on_device:
+            self._torch_order()   # the caller may have rewritten comp since the last run
         check(lib.ppg_shard_run(self._h), "DecompressAll")
         return self
+
+    def copy_output(self, off, length, dst=None):
+        """Bytes [off, off+length) of the shard's decompressed output (relative to its first
+        chunk's Output) into a new uint8 numpy array, or into `dst`: a numpy array (host) or a
+        uint8 CUDA tensor on this device (device-to-device, stream-ordered after torch's stream)."""
+        if dst is None:
+            dst = np.empty(int(length), np.uint8)
+        if hasattr(dst, "data_ptr"):
+            if not (dst.is_cuda and dst.numel() >= length):
+                raise ValueError("copy_output: dst tensor must be a CUDA tensor of >= length bytes")
+            self.dev.after_torch()
+            check(lib.ppg_shard_copy_output(self._h, int(off), int(length), C.c_void_p(dst.data_ptr()), 1),
+                  "copy_output")
+        else:
+            if dst.nbytes < length:
+                raise ValueError("copy_output: dst too small")
+            check(lib.ppg_shard_copy_output(self._h, int(off), int(length), _ptr(dst), 0), "copy_output")
+        return dst
 
     @property
     def batches(self):
@@ -403,6 +468,7 @@ class Shard:
         return b
 
     def counts_to_device(self, dev_ptr):
+        self._torch_order()
         check(lib.ppg_shard_counts_to_device(self._h, C.c_void_p(int(dev_ptr))), "counts_to_device")
 
     def timing(self):

@@ -80,10 +80,13 @@ _SIGS = {
     "ppg_index_window": (vp, [vp, i32]),
     "ppg_index_offset": (vp, [vp, i32]),
     "ppg_index_free": (None, [vp]),
+    "ppg_index_validate": (C.c_int, [vp, i32, i32]),
     "ppg_device_count": (C.c_int, [P(C.c_int)]),
     "ppg_open": (C.c_int, [C.c_int, P(vp)]),
     "ppg_close": (None, [vp]),
     "ppg_ctx_stream": (vp, [vp]),
+    "ppg_ctx_wait_stream": (C.c_int, [vp, vp]),
+    "ppg_stream_wait_ctx": (C.c_int, [vp, vp]),
     "ppg_decompress_chunk": (C.c_int, [vp, vp, i32, vp, i64, vp, i64, P(i64), vp, i64, P(i64)]),
     "ppg_shard_create": (C.c_int, [vp, vp, i32, i32, vp, i64, C.c_int, i64, P(vp)]),
     "ppg_shard_free": (None, [vp]),
@@ -95,6 +98,7 @@ _SIGS = {
     "ppg_shard_copy_chunk": (C.c_int, [vp, i32, vp, i64, P(i64)]),
     "ppg_shard_copy_records": (C.c_int, [vp, i32, vp, i64, P(i64)]),
     "ppg_shard_record_base": (C.c_int, [vp, vp]),
+    "ppg_shard_copy_output": (C.c_int, [vp, i64, i64, vp, C.c_int]),
     "ppg_shard_keys": (C.c_int, [vp, vp, i64]),
     "ppg_shard_counts_to_device": (C.c_int, [vp, vp]),
     "ppg_shard_timing": (C.c_int, [vp, P(C.c_float), P(C.c_float), P(C.c_float)]),

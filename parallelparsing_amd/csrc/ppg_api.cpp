@@ -296,6 +296,25 @@ const uint8_t *ppg_index_offset(const ppg_index *ix, int32_t i) {
 
 void ppg_index_free(ppg_index *ix) { delete ix; }
 
+// What the decode kernels can take (ppg_shard_create checks it): Points ordered by Input; per
+// chunk an output length below 2^31 together with its offset carry (the kernel and the descriptors
+// index a chunk's raw bytes with 32 bits; the reference's (int)(to.Output - from.Output), Core.cs:140,
+// breaks at the same size) and a compressed span of fewer than 2^32 - 2^12 bits (the kernel's bit
+// reader is 32-bit relative to the 4096-bit line holding the chunk's first bit).
+int ppg_index_validate(const ppg_index *ix, int32_t first, int32_t n) {
+    if (!ix || first < 0 || n < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size()) return PPG_ARG_ERROR;
+    for (int32_t i = 0; i < n; i++) {
+        const PpgPoint &from = ix->pts[(size_t)first + i], &to = ix->pts[(size_t)first + i + 1];
+        if (from.input < 1 || to.input < from.input || from.bits < 0 || from.bits > 7 || to.bits < 0 || to.bits > 7)
+            return PPG_ARG_ERROR;
+        const int64_t ulen = to.output - from.output;
+        if (ulen > 0 && (uint64_t)ulen + from.offset.size() >= (1ull << 31)) return PPG_UNSUPPORTED;
+        const uint64_t b0 = (uint64_t)(8 * from.input - from.bits), b1 = (uint64_t)(8 * to.input);
+        if (b1 - (b0 & ~4095ull) >= 0xFFFFF000ull) return PPG_UNSUPPORTED;
+    }
+    return PPG_OK;
+}
+
 const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate, LDS 32 KiB ring)"; }
 
 }  // extern "C"
@@ -349,11 +368,32 @@ void ppg_close(ppg_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     ingest_free(ctx->ingest);
+    if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
 void *ppg_ctx_stream(ppg_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+// Stream-ordered handoff with a caller's stream (torch's current stream, a C# host's own): one
+// event recorded on the producer stream, waited on by the consumer stream -- no host drain.
+static int stream_order(ppg_ctx *ctx, hipStream_t producer, hipStream_t consumer) {
+    HIPCHK(hipSetDevice(ctx->device));
+    if (!ctx->handoff) HIPCHK(hipEventCreateWithFlags(&ctx->handoff, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->handoff, producer));
+    HIPCHK(hipStreamWaitEvent(consumer, ctx->handoff, 0));
+    return PPG_OK;
+}
+
+int ppg_ctx_wait_stream(ppg_ctx *ctx, void *stream) {
+    if (!ctx) return PPG_ARG_ERROR;
+    return stream_order(ctx, (hipStream_t)stream, ctx->stream);
+}
+
+int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream) {
+    if (!ctx) return PPG_ARG_ERROR;
+    return stream_order(ctx, ctx->stream, (hipStream_t)stream);
+}
 
 }  // extern "C"
 
@@ -422,6 +462,7 @@ static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int3
     const auto &P = ix->pts;
     const int64_t base_byte = P[(size_t)first].input - 1;
     if (base_byte < 0) return PPG_ARG_ERROR;
+    if (const int v = ppg_index_validate(ix, first, n); v != PPG_OK) return v;
     if (comp_len != P[(size_t)first + n].input - P[(size_t)first].input + 1) return PPG_ARG_ERROR;
     if (((uintptr_t)comp & 3) != 0) return PPG_ARG_ERROR;
     sh->first = first;
@@ -817,7 +858,22 @@ int ppg_shard_counts_to_device(ppg_shard *sh, int64_t *dev_dst) {
     HIPCHK(hipSetDevice(sh->ctx->device));
     std::vector<int64_t> c((size_t)sh->n);
     for (int32_t i = 0; i < sh->n; i++) c[(size_t)i] = (int64_t)sh->h_info[(size_t)i].records;
-    if (sh->n) HIPCHK(hipMemcpy(dev_dst, c.data(), 8 * (size_t)sh->n, hipMemcpyHostToDevice));
+    hipStream_t s = sh->ctx->stream;   // ordered after ppg_ctx_wait_stream
+    if (sh->n) HIPCHK(hipMemcpyAsync(dev_dst, c.data(), 8 * (size_t)sh->n, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PPG_OK;
+}
+
+int ppg_shard_copy_output(ppg_shard *sh, int64_t off, int64_t len, void *dst, int dst_on_device) {
+    if (!sh || !sh->ran || sh->batches.size() != 1 || off < 0 || len < 0 || (len && !dst)) return PPG_ARG_ERROR;
+    const int64_t total = sh->h_pout[(size_t)sh->n] - sh->h_pout[0];
+    if (off + len > total) return PPG_ARG_ERROR;
+    if (!len) return PPG_OK;
+    HIPCHK(hipSetDevice(sh->ctx->device));
+    hipStream_t s = sh->ctx->stream;
+    HIPCHK(hipMemcpyAsync(dst, sh->out.p + off, (size_t)len,
+                          dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return PPG_OK;
 }
 

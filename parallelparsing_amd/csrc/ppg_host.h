@@ -73,6 +73,7 @@ struct IngestState;   // host-ingest buffers kept across ppg_file_decompress_all
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t handoff = nullptr;   // ppg_ctx_wait_stream / ppg_stream_wait_ctx
     IngestState *ingest = nullptr;
     int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
     int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)

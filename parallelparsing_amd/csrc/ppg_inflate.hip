@@ -426,7 +426,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     if (k >= njobs) return;
     const PpgInflateJob J = jobs[k];
     const uint64_t out_off = J.out_off;
-    const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // host guarantees < 2^31
+    const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // < 2^31: ppg_index_validate
     const uint32_t rb0 = (uint32_t)out_off;         // ring slot of chunk position p: (rb0 + p) & RM
     const uint8_t *dict = dicts + J.dict_off;       // chunk position p < 0 is dict[32768 + p]
     const uint8_t *ob = out + (out_off & ~3ull);    // chunk position p >= 0 is ob[oa + p]
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     r.sg = 0x7FFFFFF0u;   // nothing resident: the first seek loads
     r.base = comp + w0abs;
     r.nw = (uint32_t)min(nwords > w0abs ? nwords - w0abs : 1ull, 0xFFFFFFFFull);
-    const uint32_t bit_limit = (uint32_t)min(J.bit_limit - w0abs * 32, 0xFFFFFFFFull);
+    const uint32_t bit_limit = (uint32_t)min(J.bit_limit - w0abs * 32, 0xFFFFFFFFull);   // < 2^32 - 2^12: ppg_index_validate
     rd_seek(r, S.stream, (uint32_t)(J.bit_start - w0abs * 32), lane);
 
     // lane constants of the round loop

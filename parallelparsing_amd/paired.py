@@ -29,10 +29,11 @@ def shard_keys(shard):
     n = shard.total_records
     dev = torch.device("cuda", shard.dev.device)
     keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-    # the kernel writes on the shard's own stream: torch's caching allocator may have handed out a
-    # block that kernels still queued on torch's stream read (e.g. a boolean mask freed by the caller
-    # while its gather is in flight), so let torch's stream drain first
-    torch.cuda.current_stream(dev).synchronize()
+    # the kernel writes on the ctx's stream: torch's caching allocator may have handed out a block
+    # that kernels still queued on torch's stream read (e.g. a boolean mask freed by the caller
+    # while its gather is in flight), so the ctx waits for torch's stream first (stream-ordered,
+    # ppg_ctx_wait_stream; r01 drained torch's stream from the host here)
+    shard.dev.wait_stream(torch.cuda.current_stream(dev))
     check(lib.ppg_shard_keys(shard.handle, C.c_void_p(keys.data_ptr()), n), "ppg_shard_keys")
     return keys[:n]
 

@@ -1,0 +1,54 @@
+"""bench.py's own rank launcher (the driver may start `python bench.py --gpus N` directly): with
+no WORLD_SIZE in the environment it must start N ranks through torch.distributed.run, each with
+its RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, before anything touches a GPU.  PPG_BENCH_DRYRUN
+makes every rank report its environment and exit, so this runs on the CPU."""
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    with tempfile.TemporaryDirectory() as d:
+        env.update(PPG_BENCH_DRYRUN=d, **(extra_env or {}))
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = []
+        for p in sorted(glob.glob(os.path.join(d, "rank*.json"))):
+            with open(p) as f:
+                out.append(json.load(f))
+        return out
+
+
+def test_launcher_starts_n_ranks():
+    lines = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert sorted(x["rank"] for x in lines) == [0, 1]
+    assert sorted(x["local_rank"] for x in lines) == [0, 1]
+    assert all(x["world"] == 2 for x in lines)
+    assert all(x["scaling"] == "strong" for x in lines)          # configs[3] by default for N > 1
+    assert all(x["master"].startswith("127.0.0.1:") for x in lines)
+
+
+def test_single_gpu_stays_in_process():
+    lines = _run(["--gpus", "1"])
+    assert lines == [{"rank": 0, "local_rank": 0, "world": 1, "scaling": "weak", "master": "None:None"}]
+
+
+def test_weak_flag_kept_for_n_ranks():
+    lines = _run(["--gpus", "2", "--scaling", "weak"])
+    assert [x["scaling"] for x in lines] == ["weak", "weak"]
+
+
+def test_launch_cmd_shape():
+    sys.path.insert(0, ROOT)
+    import bench
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "3"], 29511)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=8" in cmd and "127.0.0.1" in cmd and "--master-port=29511" in cmd
+    assert cmd[-3:] == ["--gpus", "8", "--steps", "3"][-3:]

@@ -4,6 +4,7 @@ import gzip
 import hashlib
 import os
 
+import numpy as np
 import pytest
 
 import parallelparsing_amd as pp
@@ -76,3 +77,38 @@ def test_errors_mirror_zexception():
     with pytest.raises(pp.PpgError) as e:
         pp.IndexIO.Deserialize("/nonexistent/x.gzi")
     assert e.value.code == -51
+
+
+def _index_with_deltas(outputs, inputs, bits=None, offset_len=None):
+    n = len(outputs)
+    bits = bits if bits is not None else [0] * n
+    offset_len = offset_len if offset_len is not None else [0] * n
+    offs = np.zeros(max(1, sum(offset_len)), np.uint8)
+    return pp.Index.from_points(np.array(outputs, np.int64), np.array(inputs, np.int64), np.array(bits, np.int32),
+                                np.zeros(n * 32768, np.uint8), np.array(offset_len, np.int32), offs[:sum(offset_len)])
+
+
+def test_validate_rejects_chunks_too_large_for_the_kernels():
+    """a chunk whose output reaches 2^31 bytes (the kernel's and the descriptors' 32-bit
+    raw index; Core.cs:140 casts the same length to int) or whose compressed span reaches 2^32 bits
+    is refused up front (PPG_UNSUPPORTED), before any device work -- never decoded short."""
+    ok = _index_with_deltas([0, 1000, (1 << 31) - 40000], [10, 500, 900])
+    ok.validate()
+    big = _index_with_deltas([0, 1000, 1000 + (1 << 31)], [10, 500, 900])
+    big.validate(0, 1)                                   # the first chunk alone is fine
+    with pytest.raises(pp.PpgError) as e:
+        big.validate()
+    assert e.value.code == -53
+    # the offset carry counts toward the raw index: 2^31 - 100 bytes + a 200-byte carry
+    carry = _index_with_deltas([0, (1 << 31) - 100], [10, 500], offset_len=[200, 0])
+    with pytest.raises(pp.PpgError) as e:
+        carry.validate()
+    assert e.value.code == -53
+    span = _index_with_deltas([0, 1000], [10, 10 + (1 << 29)])   # 2^32 compressed bits
+    with pytest.raises(pp.PpgError) as e:
+        span.validate()
+    assert e.value.code == -53
+    bad = _index_with_deltas([0, 1000], [500, 10])                # Inputs out of order
+    with pytest.raises(pp.PpgError) as e:
+        bad.validate()
+    assert e.value.code == -52
