@@ -72,6 +72,18 @@ def host_cpu_info():
     return info
 
 
+def usable_cpus():
+    """Host cores this process can actually run on: the scheduler affinity, capped by the cgroup
+    CPU quota (the GPU box shows 256 CPUs but grants a 16-CPU quota: 256 threads there measured
+    slower than 16, r02).  BASELINE.md §2's T = all host cores; nproc is reported beside it and
+    timed as a variant."""
+    info = host_cpu_info()
+    n = info["affinity"] or 1
+    if info["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(round(info["cgroup_cpu_quota"]))))
+    return n
+
+
 def _timed(fn, warm, runs):
     """BASELINE.md §2 protocol: `warm` untimed runs, then the median of `runs` timed ones."""
     for _ in range(warm):
@@ -87,7 +99,7 @@ def _timed(fn, warm, runs):
 def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
     """The oracle's threaded DecompressAll (C restatement of BatchedFASTQ over zlib 1.2.11) on a
     bounded prefix of the same file, timed on this host (rank 0, N = 1 only): T = every host core
-    (os.cpu_count()), 2 warm-ups + the median of 5, plus one thread and the
+    (usable_cpus()), 2 warm-ups + the median of 5, plus one thread, nproc threads and the
     C#-shaped consumer that materialises every record as FastqRecord does (median of 3 each)."""
     from oracle import oracle as O
     sample = min(nchunks, int(os.environ.get("PPG_CPU_SAMPLE_CHUNKS", "4096")))
@@ -101,13 +113,18 @@ def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
     # SURVEY 8d variants: one thread, and the C#-shaped consumer that materialises every record
     # into its own buffer as FastqRecord does (Parsing.cs:41-47, mode 1), on smaller prefixes
     variants = {}
-    for name, th, mode, n in (("1 thread", 1, 0, min(sample, 128)),
-                              (f"{threads} threads, records materialised", threads, 1, min(sample, 2048))):
+    nproc = min(512, os.cpu_count() or 1)   # capped for the box's process/thread limit
+    runs = [("1 thread", 1, 0, min(sample, 128)),
+            (f"{threads} threads, records materialised", threads, 1, min(sample, 2048))]
+    if nproc != threads:
+        runs.append((f"{nproc} threads (= nproc, over the {threads}-CPU quota)", nproc, 0, sample))
+    for name, th, mode, n in runs:
         (r1, _), d1, _ = _timed(lambda: O.decompress_all(gz, oi, threads=th, mode=mode, first=0, last=n), 1, 3)
         variants[name] = {"records_per_s": r1 / d1, "cores": th, "chunks": n, "seconds_median": d1}
     return {"value": recs / dt, "unit": "records/s", "cores": threads, "kind": "port",
             "sample": f"first {sample} of {nchunks} chunks ({recs:,} records, {out_bytes / 1e9:.2f} GB out) "
-                      f"of the same file, {threads} threads (= os.cpu_count()), median of 5 after 2 warm-ups: "
+                      f"of the same file, {threads} threads (every usable host core: affinity and cgroup quota), median "
+                      f"of 5 after 2 warm-ups: "
                       f"{dt:.2f} s",
             "runs_s": [round(t, 3) for t in ts], "host": host_cpu_info(),
             "decompressed_MBps": out_bytes / dt / 1e6, "variants": variants}
@@ -541,8 +558,7 @@ def main():
         except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
             line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(512, os.cpu_count() or 1)   # every host core (capped for the pid limit)
-        line["cpu_baseline"] = cpu_baseline(tf, ix_out, ix_in, nchunks, threads)
+        line["cpu_baseline"] = cpu_baseline(tf, ix_out, ix_in, nchunks, usable_cpus())
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -84,3 +84,8 @@ struct PpgSpan {          // byte range [lo, hi) of an output buffer
 #define PPG_FLAG_NO_EOB 1     // the symbol after the last output byte is not end-of-block
 #define PPG_FLAG_OVERRUN 2    // decoding consumed bits past the chunk's compressed slice
 #define PPG_FLAG_BLK_FULL 16  // CreateIndex pass 1: more block ends than blk_cap
+
+// CRC-32 of the GPU CreateIndex's exact output (ppg_crc_kernel): one lane per kCrcSub bytes, one
+// wave (64 lanes) per kCrcSeg bytes
+constexpr uint32_t kCrcSub = 16384;
+constexpr uint32_t kCrcSeg = 64 * kCrcSub;

@@ -308,3 +308,63 @@ hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan 
     hipLaunchKernelGGL(ppg_at_stats_kernel, dim3(n), dim3(64), 0, s, out, spans, st, n);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// CRC-32 of the exact output (GPU CreateIndex, RFC 1952 trailer check that zlib's gzip mode makes
+// in the reference's CreateIndex, Core.cs:30 inflateInit2(47) -> Z_DATA_ERROR at Core.cs:68-74).
+//
+// Register algebra (reflected CRC-32, poly 0xEDB88320): R(c, A||B) = R(0, B) ^ Z(c, |B|), where
+// Z(c, n) = R(c, n zero bytes) is linear in c.  A batch of n bytes is viewed front-padded with
+// zeros to a multiple of kCrcSeg (R(0, zeros||A) = R(0, A)); one wave per kCrcSeg virtual bytes,
+// one lane per kCrcSub of them: lane registers start at 0, the wave folds them in order with the
+// table of Z(., kCrcSub) (4 x 256 u32), and the host folds the segments with Z(., kCrcSeg) and the
+// batches with zlib's crc32_combine (= Z(c1, n2) ^ c2).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ppg_crc_kernel(const uint8_t *__restrict__ out, uint64_t n, uint64_t pad,
+                                                     const uint32_t *__restrict__ tabs, uint32_t *__restrict__ seg_raw,
+                                                     uint64_t nseg) {
+    __shared__ uint32_t T[4][256];   // slicing-by-4 byte tables
+    __shared__ uint32_t Z[4][256];   // Z(., kCrcSub) by byte lane
+    __shared__ uint32_t part[64];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 1024; i += 64) {
+        (&T[0][0])[i] = tabs[i];
+        (&Z[0][0])[i] = tabs[1024 + i];
+    }
+    __syncthreads();
+    const uint64_t w = blockIdx.x;
+    if (w >= nseg) return;
+    // this lane's real byte range [a, b) of the batch (virtual v -> real v - pad)
+    const uint64_t v0 = w * (uint64_t)kCrcSeg + (uint64_t)lane * kCrcSub;
+    const uint64_t a = v0 + kCrcSub <= pad ? 0 : (v0 < pad ? 0 : v0 - pad);
+    const uint64_t b = v0 + kCrcSub <= pad ? 0 : min(n, v0 + kCrcSub - pad);
+    uint32_t c = 0;
+    uint64_t p = a;
+    auto byte = [&](uint32_t x) { c = T[0][(c ^ x) & 255] ^ (c >> 8); };
+    for (; p < b && (p & 15); p++) byte(out[p]);
+    for (; p + 16 <= b; p += 16) {
+        const uint4 q = *(const uint4 *)(out + p);
+        const uint32_t ws[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t x = c ^ ws[j];
+            c = T[3][x & 255] ^ T[2][(x >> 8) & 255] ^ T[1][(x >> 16) & 255] ^ T[0][x >> 24];
+        }
+    }
+    for (; p < b; p++) byte(out[p]);
+    part[lane] = c;
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t r = 0;
+        for (int i = 0; i < 64; i++)
+            r = (Z[0][r & 255] ^ Z[1][(r >> 8) & 255] ^ Z[2][(r >> 16) & 255] ^ Z[3][r >> 24]) ^ part[i];
+        seg_raw[w] = r;
+    }
+}
+
+hipError_t ppg_launch_crc(hipStream_t s, const uint8_t *out, uint64_t n, uint64_t pad, const uint32_t *tabs,
+                          uint32_t *seg_raw, uint64_t nseg) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(ppg_crc_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, out, n, pad, tabs, seg_raw, nseg);
+    return hipGetLastError();
+}

@@ -29,8 +29,11 @@
 //
 // Scope: single-member gzip (the reference's input).  A zlib-wrapped stream, a
 // multi-member file or trailing bytes return PPG_UNSUPPORTED (ppg_index_build_file handles them).
-// The trailer's ISIZE is checked; its CRC-32 is not (zlib would also reject a bad CRC).
+// The trailer's ISIZE and CRC-32 are checked as zlib's gzip mode does (Core.cs:30 inflateInit2(47)):
+// a mismatch is PPG_DATA_ERROR.  The CRC is computed on the GPU over each pass-2 batch
+// (ppg_crc_kernel) and folded on the host (crc_fold below).
 #include "ppg_host.h"
+#include <zlib.h>
 #include <chrono>
 #include <memory>
 #include <fcntl.h>
@@ -49,6 +52,8 @@ hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *d
 hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan *spans, PpgAtStats *st, int n);
 hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
                               uint8_t *W);
+hipError_t ppg_launch_crc(hipStream_t s, const uint8_t *out, uint64_t n, uint64_t pad, const uint32_t *tabs,
+                          uint32_t *seg_raw, uint64_t nseg);
 hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const PpgInflateJob *jobs,
                                   const PpgInflateResult *res, const uint64_t *pre, PpgBlockEnd *dense, int n);
 
@@ -79,6 +84,30 @@ int64_t gzip_header_len(const uint8_t *h, int64_t n) {
     if (flg & 2) p += 2;                // FHCRC
     return p <= n ? p : -1;
 }
+
+// CRC-32 register algebra for ppg_crc_kernel (see ppg_index.hip): Z(c, n) = the register after n
+// zero bytes, linear in c, = zlib's crc32_combine(c, 0, n).  Tables give Z(., n) bytewise.
+struct CrcTables {
+    uint32_t dev[2048];                 // [0,1024): slicing-by-4 byte tables, [1024,2048): Z(., kCrcSub)
+    uint32_t seg[1024];                 // Z(., kCrcSeg), for the host fold
+    CrcTables() {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1)));
+            dev[i] = c;
+        }
+        for (int t = 1; t < 4; t++)
+            for (uint32_t i = 0; i < 256; i++) dev[256 * t + i] = (dev[256 * (t - 1) + i] >> 8) ^ dev[dev[256 * (t - 1) + i] & 255];
+        for (int k = 0; k < 4; k++)
+            for (uint32_t b = 0; b < 256; b++) {
+                dev[1024 + 256 * k + b] = (uint32_t)crc32_combine(b << (8 * k), 0, kCrcSub);
+                seg[256 * k + b] = (uint32_t)crc32_combine(b << (8 * k), 0, kCrcSeg);
+            }
+    }
+    uint32_t zseg(uint32_t r) const {
+        return seg[r & 255] ^ seg[256 + ((r >> 8) & 255)] ^ seg[512 + ((r >> 16) & 255)] ^ seg[768 + (r >> 24)];
+    }
+};
 
 struct Piece {
     uint32_t slot;                      // pass-1 job / ring / tail slot
@@ -396,6 +425,12 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     int64_t records = 0, last_at = -1, last_mark = 0;   // last_mark: output of the last Point or side point
     int batches = 0;
     uint64_t nblocks_seen = 0;
+    // CRC-32 of the output (RFC 1952 trailer), raw register R(0, output so far) folded per batch
+    static const CrcTables crc_tabs;
+    DevBuf<uint32_t> crc_dtab, crc_seg;
+    HIPCHK(crc_dtab.alloc(2048));
+    HIPCHK(hipMemcpyAsync(crc_dtab.p, crc_tabs.dev, sizeof crc_tabs.dev, hipMemcpyHostToDevice, s));
+    uint32_t crc_raw = 0;
     double t_census = 0;
     ix = ppg_index{};
     std::vector<uint8_t> zeros(kWin, 0);
@@ -430,11 +465,24 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         HIPCHK(B.gat.alloc(nbat));
         HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * nbat, hipMemcpyHostToDevice, s));
         HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, tmp.p, W.p, B.diff.p, (int)nbat));
+        // CRC-32 of the batch's output: front-padded to whole kCrcSeg segments, one wave each
+        const uint64_t nb_out = O[b1] - O[b0];
+        const uint64_t crc_pad = (kCrcSeg - nb_out % kCrcSeg) % kCrcSeg;
+        const uint64_t nseg = (nb_out + crc_pad) / kCrcSeg;
+        HIPCHK(crc_seg.alloc(std::max<uint64_t>(nseg, 1)));
+        HIPCHK(ppg_launch_crc(s, out.p, nb_out, crc_pad, crc_dtab.p, crc_seg.p, nseg));
+        std::vector<uint32_t> hseg(nseg);
+        if (nseg) HIPCHK(hipMemcpyAsync(hseg.data(), crc_seg.p, 4 * nseg, hipMemcpyDeviceToHost, s));
         std::vector<PpgInflateResult> r2(nbat);
         std::vector<uint32_t> hd(nbat);
         HIPCHK(hipMemcpyAsync(r2.data(), res2.p + b0, sizeof(PpgInflateResult) * nbat, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(hd.data(), B.diff.p, 4 * nbat, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        {
+            uint32_t r = 0;   // R(0, batch output) = fold of the segments with Z(., kCrcSeg)
+            for (uint32_t v : hseg) r = crc_tabs.zseg(r) ^ v;
+            crc_raw = (uint32_t)crc32_combine(crc_raw, r, (z_off_t)nb_out);
+        }
         for (size_t i = 0; i < nbat; i++) {
             if (r2[i].status != PPG_OK) return r2[i].status;
             if (r2[i].produced != U[b0 + i]) return PPG_DATA_ERROR;
@@ -564,7 +612,14 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     if (tpos + 8 < len) return PPG_UNSUPPORTED;       // another member or trailing bytes
     const uint32_t isize = (uint32_t)trailer[4] | ((uint32_t)trailer[5] << 8) | ((uint32_t)trailer[6] << 16) |
                            ((uint32_t)trailer[7] << 24);
-    if (isize != (uint32_t)total) return PPG_DATA_ERROR;
+    if (isize != (uint32_t)total) return PPG_DATA_ERROR;                   // zlib: "incorrect length check"
+    {
+        const uint32_t want = (uint32_t)trailer[0] | ((uint32_t)trailer[1] << 8) | ((uint32_t)trailer[2] << 16) |
+                              ((uint32_t)trailer[3] << 24);
+        // crc32(output) = R(~0, output) ^ ~0 = R(0, output) ^ Z(~0, |output|) ^ ~0
+        const uint32_t got = crc_raw ^ (uint32_t)crc32_combine(0xFFFFFFFFu, 0, (z_off_t)total) ^ 0xFFFFFFFFu;
+        if (got != want) return PPG_DATA_ERROR;                                 // zlib: "incorrect data check"
+    }
     if (last_at < 0 ? (int64_t)total > kMaxRun : (int64_t)total - 1 - last_at >= kMaxRun) return PPG_INDEX_OUT_OF_RANGE;
     {
         std::vector<uint8_t> w(kWin);

@@ -112,3 +112,13 @@ def test_validate_rejects_chunks_too_large_for_the_kernels():
     with pytest.raises(pp.PpgError) as e:
         bad.validate()
     assert e.value.code == -52
+
+
+def test_host_create_index_rejects_bad_trailer_crc():
+    """zlib's gzip mode (Core.cs:30, inflateInit2(47)) checks the trailer CRC-32: Z_DATA_ERROR."""
+    meta, gz = load_case("l6_c20")
+    crc = int.from_bytes(gz[-8:-4], "little") ^ 0x10
+    bad = gz[:-8] + crc.to_bytes(4, "little") + gz[-4:]
+    with pytest.raises(pp.PpgError) as e:
+        pp.Core.BuildDeflateIndex(bad, meta["chunksize"])
+    assert e.value.code == -3

@@ -169,6 +169,28 @@ def test_corrupt_member_is_an_error(device):
         pp.Core.BuildDeflateIndexGpu(bytes(gz[:len(gz) // 2]), 100, device=device)
 
 
+@pytest.mark.parametrize("out_capacity", [0, 1 << 20])
+def test_trailer_crc_checked_like_zlib(out_capacity, device):
+    """the reference's CreateIndex runs zlib in gzip mode (Core.cs:30), which
+    rejects a trailer CRC-32 that does not match the output (Z_DATA_ERROR, thrown at Core.cs:68-74).
+    Both CreateIndex paths return PPG_DATA_ERROR (-3); the GPU path folds per-batch CRCs, so a
+    small out_capacity (many pass-2 batches) must agree with one batch."""
+    gz = synth_gz(fastq_text(40_000, seed=21))
+    good = pp.Core.BuildDeflateIndexGpu(gz, 2000, device=device, piece_bytes=65536, out_capacity=out_capacity)
+    same_index(good, pp.Core.BuildDeflateIndex(gz, 2000))
+    if out_capacity:
+        assert pp.Core.gpu_index_stats(device)["batches"] > 4
+    for flip in (0, 7, 31):
+        crc = int.from_bytes(gz[-8:-4], "little") ^ (1 << flip)
+        bad = gz[:-8] + crc.to_bytes(4, "little") + gz[-4:]
+        for build in (lambda: pp.Core.BuildDeflateIndex(bad, 2000),
+                      lambda: pp.Core.BuildDeflateIndexGpu(bad, 2000, device=device, piece_bytes=65536,
+                                                           out_capacity=out_capacity)):
+            with pytest.raises(pp.PpgError) as e:
+                build()
+            assert e.value.code == -3
+
+
 def test_device_resident_and_file_inputs(tmp_path, device):
     import torch
     gz = synth_gz(fastq_text(50_000, seed=6))
