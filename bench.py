@@ -228,38 +228,46 @@ def create_index_run(tf, args, dev):
                               "projected_seconds_full_member": text / 1e9 / cpu_gbs}}
 
 
-def paired_run(args, dev):
-    """BASELINE configs[4]-shaped paired-end run on one GPU: two tiled members (R1 / R2 of a read
-    pair: equal spot numbers, different SRR ids and bases), chunk = 50,000, both decoded and
-    resident, every record's spot key extracted on the GPU, Q1 duplicates dropped and the pair
-    invariant checked on the device (paired.PairedFASTQ's path).  Size per file: --paired-repeats
-    segments (default ~12.5 GB gz each: both decoded outputs must stay resident for pairing)."""
+def paired_run(args, dev, world=1, rank=0, xdev=None):
+    """BASELINE configs[4]-shaped paired-end run: two tiled members (R1 / R2 of a read pair: equal
+    spot numbers, different SRR ids and bases), chunk = 50,000, both decoded and resident, every
+    record's spot key extracted on the GPU, Q1 duplicates dropped and the pair invariant checked
+    (paired.PairedFASTQ's path).  On N ranks each rank decodes its contiguous chunk range of BOTH
+    files (dist.partition_chunks per file); the files' record ranges do not line up across ranks,
+    so the pair check is a real exchange: paired.distributed_pair_check all-gathers the counts and
+    moves every spot key to the rank owning its pair number (all_to_all, RCCL over xGMI).  Size per
+    file: --paired-repeats segments (default: ~12.5 GB of gzip per file on one GPU -- both decoded
+    outputs must stay resident for pairing -- and configs[4]'s 25 GB per file for N > 1)."""
     import torch
     import parallelparsing_amd as pp
     from parallelparsing_amd import paired
+    from parallelparsing_amd.dist import partition_chunks
     from parallelparsing_amd.tiled import TiledFile
+    reps = args.paired_repeats or (51 if world == 1 else 102)
     t = time.time()
-    tfs = [TiledFile(args.seg_records, args.paired_repeats, 50_000, seed=m - 1, mate=m, threads=args.host_threads)
+    tfs = [TiledFile(args.seg_records, reps, 50_000, seed=m - 1, mate=m, threads=args.host_threads)
            for m in (1, 2)]
     log(f"[bench] paired input: 2 x {tfs[0].records * tfs[0].repeats:,} records, "
         f"{tfs[0].file_len / 1e9:.2f} + {tfs[1].file_len / 1e9:.2f} GB gz, built in {time.time() - t:.1f}s")
     # one ctx (= one HIP stream) per file, so the two DecompressAll passes run concurrently: at
     # chunk = 50,000 one file has only ~2.7k chunks, a third of the GPU's 8k wave slots
     ctxs = [pp.Device(dev.index), pp.Device(dev.index)]
-    args.split, _ = auto_split(args, wave_slots(dev), sum(tf.npoints - 1 for tf in tfs))
+    ranges = [partition_chunks(tf.p_input, world)[rank] for tf in tfs]
+    args.split, _ = auto_split(args, wave_slots(dev), sum(b - a for a, b in ranges))
     shards, bufs = [], []
-    for tf, ctx in zip(tfs, ctxs):
-        lo, hi = int(tf.p_input[0]) - 1, int(tf.p_input[-1])
+    for tf, ctx, (a, b) in zip(tfs, ctxs, ranges):
+        lo, hi = int(tf.p_input[a]) - 1, int(tf.p_input[b])
         comp = torch.empty(hi - lo + 256, dtype=torch.uint8, device=dev)
         comp[hi - lo:].zero_()
         tf.fill_device(comp, lo, hi)
         bufs.append(comp)
-        out_cap = int(tf.p_output[-1] - tf.p_output[0]) + (1 << 20)
-        shards.append(pp.Shard(tf.index(0, tf.npoints), comp.data_ptr(), first=0, n=tf.npoints - 1, device=ctx,
+        out_cap = int(tf.p_output[b] - tf.p_output[a]) + (1 << 20)
+        shards.append(pp.Shard(tf.index(a, b + 1), comp.data_ptr(), first=0, n=b - a, device=ctx,
                                comp_on_device=True, comp_len=hi - lo, out_capacity=out_cap))
         if args.split > 1:
-            shards[-1].set_split(*tf.side_points(0, tf.npoints, args.split))
+            shards[-1].set_split(*tf.side_points(a, b + 1, args.split))
     torch.cuda.synchronize()
+    log(f"[bench] rank {rank}: R1 chunks [{ranges[0][0]},{ranges[0][1]}), R2 chunks [{ranges[1][0]},{ranges[1][1]})")
 
     import threading
 
@@ -270,34 +278,49 @@ def paired_run(args, dev):
         for x in th:
             x.join()
         keys = [paired.dedup(paired.shard_keys(sh))[0] for sh in shards]
-        return paired.check_pairs(keys[0], keys[1])
+        if world == 1:
+            return paired.check_pairs(keys[0], keys[1])
+        npairs, bad = paired.distributed_pair_check(keys[0].to(xdev), keys[1].to(xdev))
+        if bad:
+            raise ValueError(f"{bad} mismatched pairs")
+        return npairs
 
+    import torch.distributed as dist
     for _ in range(args.warmup):
         step()
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         npairs = step()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
     assert npairs == tfs[0].records * tfs[0].repeats, (npairs, tfs[0].records * tfs[0].repeats)
     text = sum(int(tf.p_output[-1] - tf.p_output[0]) for tf in tfs)
     return {
-        "metric": "paired-end record pairs/sec (R1+R2 DecompressAll + on-GPU pair check), 1 MI355X",
+        "metric": f"paired-end record pairs/sec (R1+R2 DecompressAll + pair check), {world} MI355X",
         "value": npairs * args.steps / elapsed,
         "unit": "pairs/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (Generator-shape 150 bp read pairs, tiled single gzip members, zlib level 6)",
-        "config": {"workload": f"configs[4]-shaped: 2 x {tfs[0].file_len / 1e9:.1f} GB .fastq.gz on one GPU, "
+        "config": {"workload": f"configs[4]-shaped: 2 x {tfs[0].file_len / 1e9:.1f} GB .fastq.gz over {world} GPU(s), "
                                f"chunk=50000, pair chunks of 50,000 records",
                    "pairs": npairs, "gz_bytes": [tf.file_len for tf in tfs], "decompressed_bytes": text,
+                   "pair_check": "on-device" if world == 1 else "all_to_all of spot keys to pair owners",
                    "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
         "decompressed_MBps": text * args.steps / elapsed / 1e6,
     }
@@ -346,11 +369,51 @@ def launch_ranks(n, argv):
     return subprocess.run(cmd).returncode
 
 
+def make_comm(ctx, world, rank, backend, xdev):
+    """The count all-gather's communicator inside libppgpu (ppg_comm): RCCL from a unique id that
+    rank 0 makes and torch.distributed broadcasts (backend nccl), or the host shared-memory
+    transport for the one-GPU rehearsal (gloo).  If the library cannot make one, the bench keeps
+    going with torch.distributed's all_gather of the same counts and says so in the line."""
+    import uuid
+    import torch
+    import torch.distributed as dist
+    import parallelparsing_amd as pp
+    if backend == "nccl":
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            try:
+                uid = torch.frombuffer(bytearray(pp.Comm.unique_id()), dtype=torch.uint8)
+            except pp.PpgError as e:
+                log(f"[bench] ppg_comm_unique_id failed ({e})")
+        u = uid.to(xdev)
+        dist.broadcast(u, 0)
+        uid = bytes(u.cpu().numpy().tobytes())
+        ok = torch.tensor([0], dtype=torch.int64, device=xdev)
+        comm = None
+        if any(uid):
+            try:
+                comm = pp.Comm.rccl(ctx, world, rank, uid)
+            except pp.PpgError as e:
+                log(f"[bench] rank {rank}: ppg_comm_init failed ({e})")
+                ok += 1
+        else:
+            ok += 1
+        dist.all_reduce(ok)   # all ranks or none use the library's communicator
+        if int(ok.item()):
+            return None, "torch.distributed all_gather (libppgpu's RCCL communicator failed to initialise)"
+        return comm, "libppgpu ppg_shard_gather_counts over RCCL (ncclAllGather)"
+    names = [f"/ppg_bench_{uuid.uuid4().hex[:12]}" if rank == 0 else None]
+    dist.broadcast_object_list(names, 0)
+    return pp.Comm.host(world, rank, names[0]), "libppgpu ppg_shard_gather_counts over host shared memory (rehearsal)"
+
+
 def rccl_info(world, backend):
     """The communicator the run actually used (reported in the line)."""
     import torch
     import torch.distributed as dist
-    info = {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None}
+    import parallelparsing_amd as pp
+    info = {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None,
+            "libppgpu_rccl_version": pp.rccl_version()}
     try:
         info["rccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
     except Exception:   # noqa: BLE001 - informational only
@@ -377,7 +440,7 @@ def main():
                     help="also time the GPU CreateIndex over the whole member (reported under 'create_index')")
     ap.add_argument("--paired", action="store_true",
                     help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
-    ap.add_argument("--paired-repeats", type=int, default=51)   # ~12.5 GB gz per file
+    ap.add_argument("--paired-repeats", type=int, default=0)   # 0: 51 (~12.5 GB gz per file) on 1 GPU, 102 for N > 1
     ap.add_argument("--tail-split", type=int, default=8,
                     help="--split 0 on a large rank: waves per chunk for its last generation of chunks (1 = off)")
     ap.add_argument("--tail-gens", type=float, default=0.5,
@@ -428,8 +491,12 @@ def main():
     from parallelparsing_amd.dist import partition_chunks, gather_counts
 
     if args.paired:
-        assert world == 1, "--paired runs on one GPU (the multi-GPU pair exchange: paired.distributed_pair_check)"
-        print(json.dumps(paired_run(args, dev)), flush=True)
+        line = paired_run(args, dev, world, rank, xdev)
+        line["communicator"] = rccl_info(world, backend)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
         return
 
     tf = build_input(args)
@@ -459,10 +526,15 @@ def main():
     log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
         f"{shard.batches} output batch(es), setup {time.time() - t:.1f}s")
     counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
+    comm, gather_via = (None, None) if world == 1 else make_comm(ctx, world, rank, backend, xdev)
+    bounds = np.array([r[0] for r in ranges] + [ranges[-1][1]], np.int32)
 
     def step():
         shard.run()
         if world > 1:
+            if comm is not None:   # the C ABI's count all-gather (ppg_shard_gather_counts)
+                c, bs, _ = pp.gather_counts(shard, comm, bounds)
+                return c, bs
             shard.counts_to_device(counts_dev.data_ptr())
             return gather_counts(counts_dev[: b - a].to(xdev), ranges, device=xdev)
         return None
@@ -544,7 +616,7 @@ def main():
                          "descriptors": 16 * local_records // shard.batches,
                          "parse_reread": 0}},   # the newline census is fused into the inflate flush
         "reference_published_rec_s": REFERENCE_REC_S,
-        "communicator": rccl_info(world, backend),
+        "communicator": dict(rccl_info(world, backend), count_gather=gather_via),
     }
     args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest
     if rank == 0 and world == 1 and (args.ingest or args.create_index):
@@ -561,6 +633,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(tf, ix_out, ix_in, nchunks, usable_cpus())
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

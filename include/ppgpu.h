@@ -213,6 +213,74 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
                             int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,
                             double *seconds);
 
+/* ======================= streamed records: BatchedFASTQ's enumerator =======================
+ * Decompressor/BatchedFASTQ.cs:29-101 (IEnumerable<FastqRecord> over a bounded record cache fed by
+ * LazyFileReader's partition queue, LazyFileReader.cs:41-97) over the GPU path, in bounded memory:
+ * chunks [first, first+n) of gz_path in batches of whole chunks of at most batch_bytes of text
+ * (0 = 1 GiB; a single larger chunk is its own batch).  Each batch is pread (`threads` readers)
+ * into pinned memory, decoded on the GPU and handed back as host memory: the chunks' raw bytes
+ * raw_k = offset_k ++ chunk_k (Parsing.cs's CombinedMemory) concatenated in `text` at raw_off[k],
+ * and the records of chunk k as desc[4*j .. 4*j+3] for j in [rec_off[k], rec_off[k+1]), each the
+ * newline positions (n1,n2,n3,n4) relative to raw_k with the field slices of ppg_shard_copy_records.
+ * While the caller walks batch k the library reads and decodes batch k+1; a batch is valid until
+ * the next ppg_cursor_next (a FastqRecord is invalid after the next MoveNext, BatchedFASTQ.cs:56).
+ * Order is canonical (chunk by chunk), not the reference's interleaving. */
+typedef struct ppg_cursor ppg_cursor;
+typedef struct {
+    int32_t first_chunk;      /* index chunk of the batch's first chunk */
+    int32_t nchunks;
+    int64_t record_base;      /* records handed out by this cursor before this batch */
+    int64_t nrecords;
+    const uint8_t *text;      /* raw_k at text + raw_off[k] */
+    const int64_t *raw_off;   /* nchunks + 1 entries */
+    const uint32_t *desc;     /* 4 per record */
+    const int64_t *rec_off;   /* nchunks + 1 entries */
+} ppg_batch;
+
+int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
+                    int64_t batch_bytes, int threads, ppg_cursor **out);
+/* PPG_OK with the next batch in *b, PPG_STREAM_END after the last one, or a ZResult error. */
+int ppg_cursor_next(ppg_cursor *c, ppg_batch *b);
+int32_t ppg_cursor_batches(const ppg_cursor *c);
+void ppg_cursor_close(ppg_cursor *c);
+
+/* ======================= multi-GPU DecompressAll (one process per GPU) =======================
+ * BatchedFASTQ's fan-out (BatchedFASTQ.cs:62-77: a task per chunk) becomes a fan-out over GPUs:
+ * rank r decodes the contiguous chunk range [bounds[r], bounds[r+1]) that ppg_partition balances
+ * by compressed bytes, with no exchange on the data path; the one collective is an all-gather of
+ * per-chunk record counts (padded to the widest range: RCCL has no all-gatherv) followed by an
+ * exclusive scan, giving every chunk its global record number.
+ *
+ * A ppg_comm is an RCCL communicator (ncclAllGather on the ctx stream, over xGMI) -- made by the
+ * library from a unique id that rank 0 creates and the host hands to every rank (ppg_comm_init),
+ * or wrapping the caller's ncclComm_t (ppg_comm_from_rccl) -- or a host shared-memory transport
+ * between processes of one machine (ppg_comm_init_host; name = "/something", unique per job):
+ * RCCL refuses two ranks on one GPU, so that is how the N > 1 path is rehearsed on one GPU.
+ * librccl is loaded at run time (dlopen librccl.so.1: the copy already in the process, if any).
+ * A rank that fails still joins the gather, and every rank then returns the first failing
+ * rank's status, so an error never leaves the others waiting. */
+typedef struct ppg_comm ppg_comm;
+#define PPG_COMM_ID_BYTES 128
+int ppg_comm_unique_id(uint8_t *id);   /* PPG_COMM_ID_BYTES bytes (ncclGetUniqueId) */
+int ppg_comm_init(ppg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id, ppg_comm **out);
+int ppg_comm_from_rccl(ppg_ctx *ctx, void *nccl_comm, int32_t nranks, int32_t rank, ppg_comm **out);
+int ppg_comm_init_host(int32_t nranks, int32_t rank, const char *name, ppg_comm **out);
+int ppg_comm_rank(const ppg_comm *c, int32_t *rank, int32_t *nranks);
+void ppg_comm_free(ppg_comm *c);
+int ppg_rccl_version(int *version);    /* ncclGetVersion of the librccl in use */
+
+/* bounds[0..nranks]: rank r owns chunks [bounds[r], bounds[r+1]) of [first, first+n) */
+int ppg_partition(const ppg_index *ix, int32_t first, int32_t n, int32_t nranks, int32_t *bounds);
+/* After ppg_shard_run of this rank's shard (chunks [bounds[rank], bounds[rank+1])): the count
+ * all-gather + scan.  counts / bases (may be NULL): bounds[nranks] - bounds[0] entries. */
+int ppg_shard_gather_counts(ppg_shard *sh, ppg_comm *comm, const int32_t *bounds, int64_t *counts, int64_t *bases,
+                            int64_t *total_records);
+/* The whole path for a C# host's BatchedFASTQ.Count() over N GPUs: partition the index's chunks,
+ * pread this rank's compressed range from gz_path, decode it (out_capacity as ppg_shard_create),
+ * gather.  counts / bases (may be NULL): Count-1 entries in canonical order. */
+int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, const char *gz_path,
+                            int64_t out_capacity, int64_t *counts, int64_t *bases, int64_t *total_records);
+
 /* Library build string (kernel ISA, version). */
 const char *ppg_version(void);
 

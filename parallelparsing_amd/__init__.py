@@ -18,7 +18,7 @@ import os
 
 import numpy as np
 
-from ._lib import lib, check, PpgError, PPG_NO_DEVICE, synth  # noqa: F401
+from ._lib import lib, check, PpgError, PPG_NO_DEVICE, PPG_STREAM_END, PpgBatch, synth  # noqa: F401
 
 WINSIZE = 32768
 CHUNK = 16384
@@ -477,6 +477,94 @@ class Shard:
         return {"inflate_ms": a.value, "parse_ms": b.value, "total_ms": c.value}
 
 
+class Comm:
+    """ppg_comm: the communicator of multi-GPU DecompressAll's count all-gather (include/ppgpu.h).
+
+    Comm.rccl(device, nranks, rank, uid)  RCCL, from a PPG_COMM_ID_BYTES id made by
+                                          Comm.unique_id() on rank 0 and handed to every rank
+    Comm.host(nranks, rank, name)         shared memory between processes of one machine (the
+                                          one-GPU rehearsal: RCCL refuses two ranks on one GPU)"""
+
+    def __init__(self, handle, device=None):
+        self._h = C.c_void_p(handle)
+        self.dev = device
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * 128)()
+        check(lib.ppg_comm_unique_id(buf), "ppg_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, device, nranks, rank, uid):
+        h = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib.ppg_comm_init(device.handle, int(nranks), int(rank), buf, C.byref(h)), "ppg_comm_init")
+        return cls(h.value, device)
+
+    @classmethod
+    def host(cls, nranks, rank, name):
+        h = C.c_void_p()
+        check(lib.ppg_comm_init_host(int(nranks), int(rank), name.encode(), C.byref(h)), "ppg_comm_init_host")
+        return cls(h.value)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def rank_size(self):
+        r, n = C.c_int32(), C.c_int32()
+        check(lib.ppg_comm_rank(self._h, C.byref(r), C.byref(n)), "ppg_comm_rank")
+        return r.value, n.value
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.ppg_comm_free(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def rccl_version():
+    v = C.c_int()
+    return v.value if lib.ppg_rccl_version(C.byref(v)) == 0 else None
+
+
+def partition(index, nranks, first=0, n=None):
+    """ppg_partition: contiguous chunk ranges balanced by compressed bytes -> bounds[nranks + 1]."""
+    if n is None:
+        n = index.Count - 1 - first
+    b = np.zeros(nranks + 1, np.int32)
+    check(lib.ppg_partition(index.handle, int(first), int(n), int(nranks), _ptr(b)), "ppg_partition")
+    return b
+
+
+def gather_counts(shard, comm, bounds):
+    """ppg_shard_gather_counts: (counts, bases, total) of every chunk of [bounds[0], bounds[-1])."""
+    bounds = np.ascontiguousarray(bounds, np.int32)
+    m = int(bounds[-1] - bounds[0])
+    counts, bases = np.zeros(max(m, 1), np.int64), np.zeros(max(m, 1), np.int64)
+    tot = C.c_int64()
+    check(lib.ppg_shard_gather_counts(shard.handle, comm.handle, _ptr(bounds), _ptr(counts), _ptr(bases),
+                                      C.byref(tot)), "ppg_shard_gather_counts")
+    return counts[:m], bases[:m], tot.value
+
+
+def dist_decompress_all(index, gzip_path, comm, device=None, out_capacity=0):
+    """ppg_dist_decompress_all: this rank's share of the file decoded, counts gathered over comm.
+    Returns (counts, bases, total) over every chunk of the index."""
+    dev = device or Device.default()
+    m = index.Count - 1
+    counts, bases = np.zeros(max(m, 1), np.int64), np.zeros(max(m, 1), np.int64)
+    tot = C.c_int64()
+    check(lib.ppg_dist_decompress_all(dev.handle, comm.handle, index.handle, os.fsencode(gzip_path),
+                                      int(out_capacity), _ptr(counts), _ptr(bases), C.byref(tot)),
+          "ppg_dist_decompress_all")
+    return counts[:m], bases[:m], tot.value
+
+
 def decompress_file(index, gzip_path, first=0, n=None, piece_bytes=8 << 30, threads=8, device=None):
     """DecompressAll of chunks [first, first+n) straight from a .gz file (ppg_file_decompress_all):
     reader threads pread ~piece_bytes pieces into pinned buffers, H2D overlaps the decode of the
@@ -492,6 +580,74 @@ def decompress_file(index, gzip_path, first=0, n=None, piece_bytes=8 << 30, thre
                                       int(piece_bytes), int(threads), _ptr(rec), C.byref(tot), C.byref(sec)),
           "decompress_file")
     return rec[:n], tot.value, sec.value
+
+
+class Cursor:
+    """Bounded-memory record streaming (ppg_cursor): chunks [first, first+n) of a .gz file in
+    batches of whole chunks of at most batch_bytes of text, read and decoded on the GPU while the
+    previous batch is consumed.  Iterating yields Batch objects; a batch's arrays are views of the
+    library's pinned buffers and stay valid only until the next batch is requested (as a
+    FastqRecord is invalid after the next MoveNext, BatchedFASTQ.cs:56)."""
+
+    def __init__(self, index, gzip_path, first=0, n=None, batch_bytes=1 << 30, threads=8, device=None):
+        self.index = index
+        self.dev = device or Device.default()
+        if n is None:
+            n = index.Count - 1 - first
+        h = C.c_void_p()
+        check(lib.ppg_cursor_open(self.dev.handle, index.handle, os.fsencode(gzip_path), int(first), int(n),
+                                  int(batch_bytes), int(threads), C.byref(h)), "ppg_cursor_open")
+        self._h = h
+
+    def __del__(self):
+        self.close()
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.ppg_cursor_close(h)
+            self._h = None
+
+    @property
+    def batches(self):
+        return lib.ppg_cursor_batches(self._h)
+
+    def next_batch(self):
+        b = PpgBatch()
+        rc = lib.ppg_cursor_next(self._h, C.byref(b))
+        if rc == PPG_STREAM_END:
+            return None
+        check(rc, "ppg_cursor_next")
+        return Batch(b)
+
+    def __iter__(self):
+        while True:
+            b = self.next_batch()
+            if b is None:
+                return
+            yield b
+
+
+class Batch:
+    """One ppg_batch: text (uint8), raw_off / rec_off (int64, nchunks + 1), desc (nrecords x 4)."""
+
+    def __init__(self, b):
+        self.first_chunk, self.nchunks = b.first_chunk, b.nchunks
+        self.record_base, self.nrecords = b.record_base, b.nrecords
+        self.raw_off = np.ctypeslib.as_array(b.raw_off, (b.nchunks + 1,))
+        self.rec_off = np.ctypeslib.as_array(b.rec_off, (b.nchunks + 1,))
+        nt = int(self.raw_off[-1])
+        self.text = np.ctypeslib.as_array(C.cast(b.text, C.POINTER(C.c_uint8)), (max(nt, 1),))[:nt]
+        nd = 4 * int(b.nrecords)
+        self.desc = np.ctypeslib.as_array(b.desc, (max(nd, 1),))[:nd].reshape(-1, 4)
+
+    def raw(self, k):
+        """raw_k = offset_k ++ chunk_k of the batch's k-th chunk."""
+        return self.text[self.raw_off[k]:self.raw_off[k + 1]]
+
+    def records(self, k):
+        """Descriptors (n, 4) of the batch's k-th chunk."""
+        return self.desc[self.rec_off[k]:self.rec_off[k + 1]]
 
 
 class BatchedFASTQ:
@@ -530,12 +686,19 @@ class BatchedFASTQ:
                                       threads=16 if self.enable_ssd_optimization else 8)
         return total
 
+    batch_bytes = 1 << 30   # text per streamed batch (ppg_cursor): host memory stays ~2x this
+
     def __iter__(self):
-        sh = self._run()
-        for k in range(sh.n):
-            off = self.index[k].offset
-            raw = bytes(off) + sh.chunk_bytes(k).tobytes()
-            yield from records_from_descriptors(raw, sh.chunk_records(k))
+        """Records streamed through ppg_cursor in bounded memory, canonical chunk order; each
+        batch's bytes are copied out before the next one is requested."""
+        cur = Cursor(self.index, self.gzip_path, batch_bytes=self.batch_bytes,
+                     threads=16 if self.enable_ssd_optimization else 8, device=self.dev)
+        try:
+            for b in cur:
+                for k in range(b.nchunks):
+                    yield from records_from_descriptors(b.raw(k).tobytes(), b.records(k))
+        finally:
+            cur.close()
 
     def Dispose(self):
         self._shard = None

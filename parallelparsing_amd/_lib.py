@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("PPG_LIB_PATH") or os.path.join(_HERE, "libppgpu.so")
 SYNTH_PATH = os.path.join(_HERE, "libppgsynth.so")
 
 PPG_OK = 0
+PPG_STREAM_END = 1
 PPG_DATA_ERROR = -3
 PPG_BUF_ERROR = -5
 PPG_INDEX_OUT_OF_RANGE = -50
@@ -104,7 +105,28 @@ _SIGS = {
     "ppg_shard_timing": (C.c_int, [vp, P(C.c_float), P(C.c_float), P(C.c_float)]),
     "ppg_file_decompress_all": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, vp, P(i64), P(C.c_double)]),
     "ppg_version": (C.c_char_p, []),
+    "ppg_cursor_open": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, P(vp)]),
+    "ppg_cursor_next": (C.c_int, [vp, vp]),
+    "ppg_cursor_batches": (i32, [vp]),
+    "ppg_cursor_close": (None, [vp]),
+    "ppg_comm_unique_id": (C.c_int, [vp]),
+    "ppg_comm_init": (C.c_int, [vp, i32, i32, vp, P(vp)]),
+    "ppg_comm_from_rccl": (C.c_int, [vp, vp, i32, i32, P(vp)]),
+    "ppg_comm_init_host": (C.c_int, [i32, i32, C.c_char_p, P(vp)]),
+    "ppg_comm_rank": (C.c_int, [vp, P(i32), P(i32)]),
+    "ppg_comm_free": (None, [vp]),
+    "ppg_rccl_version": (C.c_int, [P(C.c_int)]),
+    "ppg_partition": (C.c_int, [vp, i32, i32, i32, vp]),
+    "ppg_shard_gather_counts": (C.c_int, [vp, vp, vp, vp, vp, P(i64)]),
+    "ppg_dist_decompress_all": (C.c_int, [vp, vp, vp, C.c_char_p, i64, vp, vp, P(i64)]),
 }
+
+
+class PpgBatch(C.Structure):
+    """ppg_batch (include/ppgpu.h)."""
+    _fields_ = [("first_chunk", C.c_int32), ("nchunks", C.c_int32), ("record_base", C.c_int64),
+                ("nrecords", C.c_int64), ("text", C.c_void_p), ("raw_off", C.POINTER(C.c_int64)),
+                ("desc", C.POINTER(C.c_uint32)), ("rec_off", C.POINTER(C.c_int64))]
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
     _f.restype = _res

@@ -398,48 +398,7 @@ int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream) {
 }  // extern "C"
 
 // ====================================== shard ======================================
-struct ppg_shard {
-    ppg_ctx *ctx = nullptr;
-    int32_t first = 0, n = 0;
-    // compressed file range [Index[first].Input-1, Index[first+n].Input-1]
-    DevBuf<uint8_t> comp_own;
-    const uint8_t *comp = nullptr;
-    int64_t comp_len = 0;
-    uint64_t nwords = 0;
-    DevBuf<PpgInflateJob> jobs;
-    DevBuf<uint8_t> dicts;
-    DevBuf<uint8_t> offs;
-    DevBuf<PpgOffsetRef> oref;
-    DevBuf<PpgInflateResult> res;
-    DevBuf<PpgParseInfo> info;
-    DevBuf<uint64_t> base;     // record base within the batch
-    DevBuf<uint64_t> total;
-    DevBuf<uint8_t> out;
-    DevBuf<uint32_t> recs;
-    DevBuf<uint32_t> nls;      // newline census of the inflate flush (PpgInflateJob::nl_off/nl_cap)
-    int64_t out_cap = 0;
-    std::vector<std::pair<int32_t, int32_t>> batches;   // chunk ranges [b0, b1) relative to first
-    std::vector<PpgInflateJob> h_jobs;
-    // results of the last run
-    std::vector<PpgInflateResult> h_res;
-    std::vector<PpgParseInfo> h_info;
-    std::vector<int64_t> h_base;   // shard-global record base per chunk
-    int64_t total_records = 0;
-    float t_inflate = 0, t_parse = 0, t_total = 0;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipStream_t stream = nullptr;   // null: the ctx stream (ppg_file_decompress_all gives each piece shard its own)
-    uint64_t *h_tot = nullptr;      // pinned: a batch's record total, read back without a stream sync
-    int ran = 0;
-    // split chunks (ppg_shard_set_split): the inflate launch runs sub-jobs, ppg_split_merge folds
-    // them back into per-chunk results and census regions
-    int32_t nsub = 0;                            // side points in use (0: one wave per chunk)
-    int64_t base_byte = 0;                       // file byte of comp[0]
-    std::vector<int64_t> h_pout;                 // Output of points first .. first + n
-    std::vector<PpgInflateJob> h_sjobs;
-    DevBuf<PpgInflateJob> sjobs;
-    DevBuf<PpgInflateResult> sres;
-    DevBuf<uint32_t> sidx;                      // chunk k = sub-jobs [sidx[k], sidx[k+1])
-};
+// struct ppg_shard: ppg_host.h
 
 extern "C" {
 
@@ -457,7 +416,7 @@ void ppg_shard_free(ppg_shard *sh) {
 // [Index[first].Input-1, Index[first+n].Input-1] is at device pointer comp (4-byte aligned,
 // readable 64 bytes past comp_len).  Device buffers are reused when large enough, so a shard can
 // be re-prepared piece after piece (ppg_file_decompress_all).
-static int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, const uint8_t *comp,
+int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, const uint8_t *comp,
                          int64_t comp_len, int64_t out_capacity, hipStream_t s) {
     const auto &P = ix->pts;
     const int64_t base_byte = P[(size_t)first].input - 1;
@@ -598,9 +557,9 @@ int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n
 
 }  // extern "C"
 
-static hipStream_t shard_stream(const ppg_shard *sh) { return sh->stream ? sh->stream : sh->ctx->stream; }
+hipStream_t shard_stream(const ppg_shard *sh) { return sh->stream ? sh->stream : sh->ctx->stream; }
 
-static void shard_reset(ppg_shard *sh) {
+void shard_reset(ppg_shard *sh) {
     sh->t_inflate = sh->t_parse = sh->t_total = 0;
     sh->h_base.assign((size_t)sh->n, 0);
     sh->total_records = 0;
@@ -610,7 +569,7 @@ static void shard_reset(ppg_shard *sh) {
 // Enqueue one batch [b0, b1) on the shard's stream, with no host synchronisation: inflate (+ the
 // fused newline census), per-chunk counts and their scan, the record total into pinned host
 // memory, then the descriptors, whose writes stop at the descriptor buffer's size.
-static int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
+int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     hipStream_t s = shard_stream(sh);
     const int nb = b1 - b0;
     HIPCHK(hipEventRecord(sh->ev[0], s));
@@ -637,7 +596,7 @@ static int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
 
 // Wait for a launched batch.  If its records did not fit the descriptor buffer (more than one
 // record per 256 output bytes), grow the buffer and write the descriptors again.
-static int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms) {
+int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms) {
     hipStream_t s = shard_stream(sh);
     const int nb = b1 - b0;
     HIPCHK(hipEventSynchronize(sh->ev[3]));
@@ -670,7 +629,7 @@ static int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms)
     return PPG_OK;
 }
 
-static int shard_finish(ppg_shard *sh, float total_ms) {
+int shard_finish(ppg_shard *sh, float total_ms) {
     hipStream_t s = shard_stream(sh);
     sh->t_total = total_ms;
     sh->h_res.resize((size_t)sh->n);
@@ -908,8 +867,6 @@ int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uin
 }  // extern "C"
 
 // ================================ host ingest (file -> GPU) ================================
-namespace {
-
 // pread [off, off+len) of fd into dst with `threads` parallel readers; false on a short read
 bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads) {
     const int64_t part = std::max<int64_t>((len + threads - 1) / threads, 1 << 20);
@@ -931,8 +888,6 @@ bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads)
     for (int v : ok) if (!v) return false;
     return true;
 }
-
-}  // namespace
 
 constexpr int kSlots = 4;     // pinned staging slots
 constexpr int kPieces = 3;   // device piece slots: one finishing, one decoding, one filling
@@ -958,10 +913,8 @@ static void ingest_free(IngestState *st) {
     delete st;
 }
 
-extern "C" {
-
 // the index's side points inside chunks [first, first+n) -> ppg_shard_set_split (host ingest)
-static int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n) {
+int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n) {
     const int64_t lo = ix->pts[(size_t)first].output, hi = ix->pts[(size_t)first + n].output;
     const auto &O = ix->side_out;
     const size_t a = (size_t)(std::upper_bound(O.begin(), O.end(), lo) - O.begin());
@@ -970,6 +923,8 @@ static int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t fi
     return ppg_shard_set_split(sh, (int32_t)(b - a), ix->side_bit.data() + a, O.data() + a,
                                ix->side_win.data() + a * kWin);
 }
+
+extern "C" {
 
 int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
                             int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,

@@ -1,0 +1,322 @@
+// ppg_comm.cpp — multi-GPU DecompressAll inside the C ABI (include/ppgpu.h, "multi-GPU").
+//
+// The reference fans DecompressAll out over threads of one host (BatchedFASTQ.cs:62-77: a task per
+// chunk pulled from LazyFileReader, records pushed into one RecordCache).  Here the fan-out is
+// over GPUs, one process (or host thread) per GPU: rank r decodes a contiguous range of chunks
+// balanced by compressed bytes (ppg_partition), with no data-path exchange, and the one collective
+// is an all-gather of per-chunk record counts followed by an exclusive scan, which gives every
+// chunk its global record number.  RCCL has no all-gatherv: counts are padded to the
+// widest range and gathered with ncclAllGather over xGMI on the ctx stream.
+//
+// Transports of a ppg_comm:
+//   RCCL      ppg_comm_init (a communicator of our own from a unique id the host distributes) or
+//             ppg_comm_from_rccl (a caller's ncclComm_t).  librccl is dlopen'ed, so a process that
+//             already holds one (torch bundles its own librccl.so.1) shares it.
+//   host      ppg_comm_init_host: POSIX shared memory between processes of one machine.  RCCL
+//             refuses two ranks on one GPU ("Duplicate GPU detected"), so this is how the N > 1
+//             path is rehearsed on a one-GPU box; the gather code above it is the same.
+#include "ppg_host.h"
+#include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+#include <atomic>
+#include <chrono>
+#include <string>
+#include <thread>
+
+namespace {
+
+struct Rccl {
+    void *h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char *(*err)(ncclResult_t) = nullptr;
+    ncclResult_t (*version)(int *) = nullptr;
+    bool load() {
+        if (h) return true;
+        // the copy already in the process (torch's), else the ROCm one
+        for (const char *name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+            h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (h) break;
+        }
+        if (!h) return false;
+        get_unique_id = (decltype(get_unique_id))dlsym(h, "ncclGetUniqueId");
+        init_rank = (decltype(init_rank))dlsym(h, "ncclCommInitRank");
+        all_gather = (decltype(all_gather))dlsym(h, "ncclAllGather");
+        destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+        err = (decltype(err))dlsym(h, "ncclGetErrorString");
+        version = (decltype(version))dlsym(h, "ncclGetVersion");
+        return get_unique_id && init_rank && all_gather && destroy && err;
+    }
+};
+
+Rccl &rccl() {
+    static Rccl r;
+    return r;
+}
+
+#define RCCLCHK(x)                                                                                  \
+    do {                                                                                            \
+        ncclResult_t r_ = (x);                                                                      \
+        if (r_ != ncclSuccess) {                                                                    \
+            fprintf(stderr, "ppgpu: %s failed: %s\n", #x, rccl().err ? rccl().err(r_) : "?");       \
+            return PPG_DEVICE_ERROR;                                                                \
+        }                                                                                           \
+    } while (0)
+
+// shared-memory all-gather between the processes of one machine (sense-reversing barrier)
+struct ShmHdr {
+    std::atomic<uint64_t> arrive;
+    std::atomic<uint64_t> gen;
+};
+constexpr int64_t kShmSlot = 8 << 20;   // bytes per rank per all-gather (1M chunk counts)
+
+}  // namespace
+
+struct ppg_comm {
+    int32_t nranks = 1, rank = 0;
+    int device = -1;                    // RCCL: the GPU the communicator was made for
+    ncclComm_t nccl = nullptr;
+    bool own_nccl = false;
+    // host transport
+    std::string shm_name;
+    ShmHdr *hdr = nullptr;
+    uint8_t *slots = nullptr;
+    size_t map_len = 0;
+
+    bool host() const { return hdr != nullptr; }
+
+    int barrier() {
+        const uint64_t g = hdr->gen.load(std::memory_order_acquire);
+        if (hdr->arrive.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint64_t)nranks) {
+            hdr->arrive.store(0, std::memory_order_relaxed);
+            hdr->gen.store(g + 1, std::memory_order_release);
+            return PPG_OK;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hdr->gen.load(std::memory_order_acquire) == g) {
+            std::this_thread::yield();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(300)) return PPG_IO_ERROR;
+        }
+        return PPG_OK;
+    }
+
+    // host memory in, host memory out: recv = nranks * bytes
+    int host_all_gather(const void *send, void *recv, int64_t bytes) {
+        if (bytes > kShmSlot) return PPG_UNSUPPORTED;
+        memcpy(slots + (size_t)rank * kShmSlot, send, (size_t)bytes);
+        if (int rc = barrier()) return rc;
+        for (int32_t r = 0; r < nranks; r++) memcpy((uint8_t *)recv + (size_t)r * bytes, slots + (size_t)r * kShmSlot,
+                                                    (size_t)bytes);
+        return barrier();   // nobody overwrites a slot before every rank has read it
+    }
+};
+
+extern "C" {
+
+int ppg_comm_unique_id(uint8_t *id) {
+    if (!id) return PPG_ARG_ERROR;
+    if (!rccl().load()) return PPG_UNSUPPORTED;
+    ncclUniqueId u;
+    RCCLCHK(rccl().get_unique_id(&u));
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return PPG_OK;
+}
+
+int ppg_comm_init(ppg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id, ppg_comm **out) {
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return PPG_ARG_ERROR;
+    if (!rccl().load()) return PPG_UNSUPPORTED;
+    HIPCHK(hipSetDevice(ctx->device));
+    auto c = std::make_unique<ppg_comm>();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = ctx->device;
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    RCCLCHK(rccl().init_rank(&c->nccl, nranks, u, rank));
+    c->own_nccl = true;
+    *out = c.release();
+    return PPG_OK;
+}
+
+int ppg_comm_from_rccl(ppg_ctx *ctx, void *nccl_comm, int32_t nranks, int32_t rank, ppg_comm **out) {
+    if (!ctx || !nccl_comm || !out || nranks < 1 || rank < 0 || rank >= nranks) return PPG_ARG_ERROR;
+    if (!rccl().load()) return PPG_UNSUPPORTED;
+    auto c = std::make_unique<ppg_comm>();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = ctx->device;
+    c->nccl = (ncclComm_t)nccl_comm;
+    *out = c.release();
+    return PPG_OK;
+}
+
+int ppg_comm_init_host(int32_t nranks, int32_t rank, const char *name, ppg_comm **out) {
+    if (!name || !out || nranks < 1 || rank < 0 || rank >= nranks || name[0] != '/') return PPG_ARG_ERROR;
+    auto c = std::make_unique<ppg_comm>();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->shm_name = name;
+    c->map_len = 64 + (size_t)nranks * kShmSlot;
+    const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return PPG_IO_ERROR;
+    if (ftruncate(fd, (off_t)c->map_len) != 0) { close(fd); return PPG_IO_ERROR; }
+    void *p = mmap(nullptr, c->map_len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return PPG_IO_ERROR;
+    c->hdr = (ShmHdr *)p;
+    c->slots = (uint8_t *)p + 64;
+    // every rank has mapped the segment (zero-filled by ftruncate) before any gather starts
+    if (int rc = c->barrier()) { munmap(p, c->map_len); return rc; }
+    *out = c.release();
+    return PPG_OK;
+}
+
+void ppg_comm_free(ppg_comm *c) {
+    if (!c) return;
+    if (c->nccl && c->own_nccl) {
+        if (c->device >= 0) (void)hipSetDevice(c->device);
+        (void)rccl().destroy(c->nccl);
+    }
+    if (c->hdr) {
+        munmap((void *)c->hdr, c->map_len);
+        if (c->rank == 0) shm_unlink(c->shm_name.c_str());
+    }
+    delete c;
+}
+
+int ppg_comm_rank(const ppg_comm *c, int32_t *rank, int32_t *nranks) {
+    if (!c) return PPG_ARG_ERROR;
+    if (rank) *rank = c->rank;
+    if (nranks) *nranks = c->nranks;
+    return PPG_OK;
+}
+
+int ppg_rccl_version(int *version) {
+    if (!version) return PPG_ARG_ERROR;
+    if (!rccl().load() || !rccl().version) return PPG_UNSUPPORTED;
+    RCCLCHK(rccl().version(version));
+    return PPG_OK;
+}
+
+// Contiguous chunk ranges balanced by compressed bytes (chunk k reads Input[k+1] - Input[k] + 1
+// bytes, LazyFileReader.cs:64): rank r owns chunks [bounds[r], bounds[r+1]) of [first, first+n).
+int ppg_partition(const ppg_index *ix, int32_t first, int32_t n, int32_t nranks, int32_t *bounds) {
+    if (!ix || !bounds || nranks < 1 || first < 0 || n < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
+        return PPG_ARG_ERROR;
+    const auto &P = ix->pts;
+    std::vector<double> cum((size_t)n + 1, 0.0);
+    for (int32_t k = 0; k < n; k++)
+        cum[(size_t)k + 1] = cum[(size_t)k] + (double)(P[(size_t)first + k + 1].input - P[(size_t)first + k].input + 1);
+    bounds[0] = first;
+    for (int32_t r = 1; r < nranks; r++) {
+        const double target = cum[(size_t)n] * r / nranks;
+        int32_t k = (int32_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+        k = std::min(std::max(k, bounds[r - 1] - first), n);
+        bounds[r] = first + k;
+    }
+    bounds[nranks] = first + n;
+    return PPG_OK;
+}
+
+}  // extern "C"
+
+// The count all-gather: every rank contributes `local` (its chunks' record counts) and its status;
+// a rank that failed still takes part (the others would wait for it forever), and every rank
+// returns the first failing rank's status.  ctx may be NULL for a host-transport comm.
+static int gather_counts(ppg_comm *comm, ppg_ctx *ctx, const std::vector<int64_t> &local, int status,
+                         const int32_t *bounds, int64_t *counts, int64_t *bases, int64_t *total_records) {
+    const int32_t R = comm->nranks;
+    int32_t width = 1;
+    for (int32_t r = 0; r < R; r++) {
+        if (bounds[r + 1] < bounds[r]) return PPG_ARG_ERROR;
+        width = std::max(width, bounds[r + 1] - bounds[r]);
+    }
+    const int32_t W = width + 1;                       // + the rank's status
+    std::vector<int64_t> send((size_t)W, 0), recv((size_t)W * R, 0);
+    std::copy(local.begin(), local.end(), send.begin());
+    send[(size_t)width] = status;
+    if (comm->host()) {
+        if (int rc = comm->host_all_gather(send.data(), recv.data(), 8 * (int64_t)W)) return rc;
+    } else {
+        if (!ctx || comm->device != ctx->device) return PPG_ARG_ERROR;
+        HIPCHK(hipSetDevice(ctx->device));
+        hipStream_t s = ctx->stream;
+        DevBuf<int64_t> d;
+        HIPCHK(d.alloc((size_t)W * (R + 1)));
+        HIPCHK(hipMemcpyAsync(d.p, send.data(), 8 * (size_t)W, hipMemcpyHostToDevice, s));
+        RCCLCHK(rccl().all_gather(d.p, d.p + W, (size_t)W, ncclInt64, comm->nccl, s));
+        HIPCHK(hipMemcpyAsync(recv.data(), d.p + W, 8 * (size_t)W * R, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    for (int32_t r = 0; r < R; r++)
+        if (recv[(size_t)r * W + width] != 0) return (int)recv[(size_t)r * W + width];
+    int64_t run = 0;
+    size_t o = 0;
+    for (int32_t r = 0; r < R; r++)
+        for (int32_t i = 0; i < bounds[r + 1] - bounds[r]; i++, o++) {
+            const int64_t c = recv[(size_t)r * W + i];
+            if (counts) counts[o] = c;
+            if (bases) bases[o] = run;
+            run += c;
+        }
+    if (total_records) *total_records = run;
+    return PPG_OK;
+}
+
+extern "C" {
+
+// After ppg_shard_run on every rank (rank r's shard = chunks [bounds[r], bounds[r+1])): one
+// all-gather of the per-chunk record counts, padded to the widest range, then the exclusive scan.
+// counts / bases (may be NULL) receive bounds[nranks] - bounds[0] entries in canonical order.
+int ppg_shard_gather_counts(ppg_shard *sh, ppg_comm *comm, const int32_t *bounds, int64_t *counts, int64_t *bases,
+                            int64_t *total_records) {
+    if (!sh || !comm || !bounds) return PPG_ARG_ERROR;
+    int status = PPG_OK;
+    std::vector<int64_t> local;
+    if (!sh->ran || bounds[comm->rank + 1] - bounds[comm->rank] != sh->n) {
+        status = PPG_ARG_ERROR;                        // still take part: the other ranks wait
+    } else {
+        local.resize((size_t)sh->n);
+        for (int32_t i = 0; i < sh->n; i++) local[(size_t)i] = (int64_t)sh->h_info[(size_t)i].records;
+    }
+    const int rc = gather_counts(comm, sh->ctx, local, status, bounds, counts, bases, total_records);
+    return status != PPG_OK ? status : rc;
+}
+
+// Multi-GPU DecompressAll of a .gz file (BatchedFASTQ over every chunk, fanned out over ranks):
+// this rank's chunk range (ppg_partition over the comm), its compressed bytes pread from the file
+// into HBM, decoded in batches of out_capacity (0: at once), then the count all-gather.  counts /
+// bases (may be NULL) get one entry per chunk of the index in canonical order.
+int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, const char *gz_path,
+                            int64_t out_capacity, int64_t *counts, int64_t *bases, int64_t *total_records) {
+    if (!ctx || !comm || !ix || !gz_path || ix->pts.size() < 1) return PPG_ARG_ERROR;
+    const int32_t n = (int32_t)ix->pts.size() - 1;
+    std::vector<int32_t> bounds((size_t)comm->nranks + 1);
+    if (int rc = ppg_partition(ix, 0, n, comm->nranks, bounds.data())) return rc;
+    const int32_t a = bounds[(size_t)comm->rank], b = bounds[(size_t)comm->rank + 1];
+    const int fd = open(gz_path, O_RDONLY);
+    struct FdClose { int fd; ~FdClose() { if (fd >= 0) close(fd); } } fdc{fd};
+    const int64_t lo = ix->pts[(size_t)a].input - 1, len = ix->pts[(size_t)b].input - ix->pts[(size_t)a].input + 1;
+    PinnedBuf pin;
+    int rc = fd < 0 ? PPG_IO_ERROR
+             : hipSetDevice(ctx->device) == hipSuccess && pin.alloc((size_t)std::max<int64_t>(len, 1)) == hipSuccess
+                 ? PPG_OK : PPG_DEVICE_ERROR;
+    if (rc == PPG_OK && len > 0 && !pread_parallel(fd, pin.p, lo, len, 8)) rc = PPG_IO_ERROR;
+    ppg_shard *sh = nullptr;
+    if (rc == PPG_OK) rc = ppg_shard_create(ctx, ix, a, b - a, pin.p, len, 0, out_capacity, &sh);
+    if (rc == PPG_OK) rc = ppg_shard_run(sh);
+    std::vector<int64_t> local((size_t)(b - a), 0);
+    if (rc == PPG_OK)
+        for (int32_t i = 0; i < b - a; i++) local[(size_t)i] = (int64_t)sh->h_info[(size_t)i].records;
+    ppg_shard_free(sh);
+    // every rank gathers, failed or not: a failure is everyone's result, never a hang
+    const int grc = gather_counts(comm, ctx, local, rc, bounds.data(), counts, bases, total_records);
+    return rc != PPG_OK ? rc : grc;
+}
+
+}  // extern "C"

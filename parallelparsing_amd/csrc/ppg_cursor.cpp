@@ -1,0 +1,178 @@
+// ppg_cursor.cpp — bounded-memory record streaming of DecompressAll through the C ABI.
+//
+// The reference's BatchedFASTQ (Decompressor/BatchedFASTQ.cs:29-101) hands out records from a
+// bounded cache (RECORD_CACHE_MAX_LENGTH = 20000, :40) fed by a partition queue of at most 32
+// (LazyFileReader.cs:12-14), so a file of any size streams through fixed memory.  ppg_cursor is
+// that surface over the GPU path: the file is cut into batches of whole chunks of at most
+// batch_bytes of text; each batch is read (pread into pinned memory), copied to HBM, decoded
+// (inflate + record scan, the DecompressAll kernels) and brought back as the chunks' raw bytes
+// (offset_k ++ chunk_k, Parsing.cs's CombinedMemory) plus the record descriptors.  Two slots
+// alternate: while the caller walks batch k, batch k+1 is read and decoded on the other slot's
+// stream.  A batch stays valid until the next ppg_cursor_next call (the reference's records are
+// likewise invalid after the next MoveNext, BatchedFASTQ.cs:56 / SURVEY Q9).  Order is canonical
+// (chunk 0's records, then chunk 1's, ...), not the reference's interleaving.
+#include "ppg_host.h"
+#include <fcntl.h>
+#include <unistd.h>
+#include <thread>
+
+namespace {
+
+struct Slot {
+    ppg_shard sh;                       // device state of the batch (its own stream)
+    DevBuf<uint8_t> dcomp;              // the batch's compressed bytes in HBM
+    PinnedBuf pcomp;                    // ... staged in pinned host memory
+    PinnedBuf text;                     // raw_k = offset_k ++ chunk_k, concatenated
+    PinnedBuf desc;                     // 4 x u32 per record
+    std::vector<int64_t> raw_off, rec_off;
+    int32_t b0 = 0, b1 = 0;             // chunks [b0, b1) relative to the cursor's first
+    int64_t nrec = 0;
+    int rc = PPG_OK;
+    std::thread worker;
+};
+
+}  // namespace
+
+struct ppg_cursor {
+    ppg_ctx *ctx = nullptr;
+    const ppg_index *ix = nullptr;
+    int fd = -1;
+    int32_t first = 0, n = 0;
+    int threads = 8;
+    std::vector<std::pair<int32_t, int32_t>> batches;
+    Slot slot[2];
+    size_t next = 0;                    // next batch to hand out
+    int64_t record_base = 0;
+
+    ~ppg_cursor() {
+        for (auto &s : slot)
+            if (s.worker.joinable()) s.worker.join();
+        (void)hipSetDevice(ctx->device);
+        for (auto &s : slot) {
+            for (auto &e : s.sh.ev) if (e) (void)hipEventDestroy(e);
+            if (s.sh.h_tot) (void)hipHostFree(s.sh.h_tot);
+            if (s.sh.stream) (void)hipStreamDestroy(s.sh.stream);
+            s.sh.h_tot = nullptr;
+            for (auto &e : s.sh.ev) e = nullptr;
+        }
+        if (fd >= 0) close(fd);
+    }
+
+    // read, decode and bring back batch i into slot s (runs on a worker thread)
+    int produce(size_t i, Slot &s) {
+        if (hipSetDevice(ctx->device) != hipSuccess) return PPG_DEVICE_ERROR;
+        const auto &P = ix->pts;
+        const int32_t a = first + batches[i].first, b = first + batches[i].second;
+        s.b0 = batches[i].first;
+        s.b1 = batches[i].second;
+        const int64_t lo = P[(size_t)a].input - 1, len = P[(size_t)b].input - P[(size_t)a].input + 1;
+        HIPCHK(s.pcomp.alloc((size_t)len));
+        if (!pread_parallel(fd, s.pcomp.p, lo, len, threads)) return PPG_IO_ERROR;
+        hipStream_t st = s.sh.stream;
+        HIPCHK(s.dcomp.alloc((size_t)len + 64));
+        HIPCHK(hipMemsetAsync(s.dcomp.p + len, 0, 64, st));
+        HIPCHK(hipMemcpyAsync(s.dcomp.p, s.pcomp.p, (size_t)len, hipMemcpyHostToDevice, st));
+        if (int rc = shard_prepare(&s.sh, ix, a, b - a, s.dcomp.p, len, 0, st)) return rc;
+        shard_reset(&s.sh);
+        float ms = 0;
+        if (int rc = batch_launch(&s.sh, 0, s.sh.n)) return rc;
+        if (int rc = batch_collect(&s.sh, 0, s.sh.n, ms)) return rc;
+        if (int rc = shard_finish(&s.sh, ms)) return rc;
+        // raw_k = offset_k ++ chunk_k (Parsing.Parse's CombinedMemory), back to pinned host memory
+        const int32_t m = b - a;
+        s.raw_off.assign((size_t)m + 1, 0);
+        for (int32_t k = 0; k < m; k++)
+            s.raw_off[(size_t)k + 1] = s.raw_off[(size_t)k] + (int64_t)P[(size_t)a + k].offset.size() +
+                                       (int64_t)s.sh.h_res[(size_t)k].produced;
+        HIPCHK(s.text.alloc((size_t)std::max<int64_t>(s.raw_off[(size_t)m], 1)));
+        s.nrec = s.sh.total_records;
+        HIPCHK(s.desc.alloc((size_t)std::max<int64_t>(16 * s.nrec, 16)));
+        for (int32_t k = 0; k < m; k++) {
+            const auto &off = P[(size_t)a + k].offset;
+            uint8_t *dst = s.text.p + s.raw_off[(size_t)k];
+            if (!off.empty()) memcpy(dst, off.data(), off.size());
+            const uint64_t got = s.sh.h_res[(size_t)k].produced;
+            if (got) HIPCHK(hipMemcpyAsync(dst + off.size(), s.sh.out.p + s.sh.h_jobs[(size_t)k].out_off, got,
+                                           hipMemcpyDeviceToHost, st));
+        }
+        if (s.nrec) HIPCHK(hipMemcpyAsync(s.desc.p, s.sh.recs.p, 16 * (size_t)s.nrec, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        s.rec_off.assign((size_t)m + 1, 0);
+        for (int32_t k = 0; k < m; k++) s.rec_off[(size_t)k + 1] = s.sh.h_base[(size_t)k] + (int64_t)s.sh.h_info[(size_t)k].records;
+        return PPG_OK;
+    }
+
+    void start(size_t i) {
+        Slot &s = slot[i & 1];
+        s.rc = PPG_OK;
+        s.worker = std::thread([this, i, &s] { s.rc = produce(i, s); });
+    }
+};
+
+extern "C" {
+
+int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
+                    int64_t batch_bytes, int threads, ppg_cursor **out) {
+    if (!ctx || !ix || !gz_path || !out || first < 0 || n < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
+        return PPG_ARG_ERROR;
+    if (int v = ppg_index_validate(ix, first, n)) return v;
+    if (batch_bytes <= 0) batch_bytes = (int64_t)1 << 30;
+    HIPCHK(hipSetDevice(ctx->device));
+    auto c = std::make_unique<ppg_cursor>();
+    c->ctx = ctx;
+    c->ix = ix;
+    c->first = first;
+    c->n = n;
+    c->threads = threads > 0 ? threads : 8;
+    c->fd = open(gz_path, O_RDONLY);
+    if (c->fd < 0) return PPG_IO_ERROR;
+    // batches: whole chunks, at most batch_bytes of raw text each (at least one chunk)
+    const auto &P = ix->pts;
+    for (int32_t a = 0; a < n;) {
+        int32_t b = a + 1;
+        int64_t raw = (P[(size_t)first + a + 1].output - P[(size_t)first + a].output) + (int64_t)P[(size_t)first + a].offset.size();
+        while (b < n) {
+            const int64_t r = (P[(size_t)first + b + 1].output - P[(size_t)first + b].output) +
+                              (int64_t)P[(size_t)first + b].offset.size();
+            if (raw + r > batch_bytes) break;
+            raw += r;
+            b++;
+        }
+        c->batches.push_back({a, b});
+        a = b;
+    }
+    for (auto &s : c->slot) {
+        s.sh.ctx = ctx;
+        HIPCHK(hipStreamCreateWithFlags(&s.sh.stream, hipStreamNonBlocking));
+    }
+    if (!c->batches.empty()) c->start(0);
+    *out = c.release();
+    return PPG_OK;
+}
+
+int ppg_cursor_next(ppg_cursor *c, ppg_batch *b) {
+    if (!c || !b) return PPG_ARG_ERROR;
+    if (c->next >= c->batches.size()) return PPG_STREAM_END;
+    Slot &s = c->slot[c->next & 1];
+    if (s.worker.joinable()) s.worker.join();
+    if (s.rc != PPG_OK) return s.rc;
+    // the other slot held the batch handed out last time: the caller is done with it
+    if (c->next + 1 < c->batches.size()) c->start(c->next + 1);
+    b->first_chunk = c->first + s.b0;
+    b->nchunks = s.b1 - s.b0;
+    b->record_base = c->record_base;
+    b->nrecords = s.nrec;
+    b->text = s.text.p;
+    b->raw_off = s.raw_off.data();
+    b->desc = (const uint32_t *)s.desc.p;
+    b->rec_off = s.rec_off.data();
+    c->record_base += s.nrec;
+    c->next++;
+    return PPG_OK;
+}
+
+int32_t ppg_cursor_batches(const ppg_cursor *c) { return c ? (int32_t)c->batches.size() : -1; }
+
+void ppg_cursor_close(ppg_cursor *c) { delete c; }
+
+}  // extern "C"

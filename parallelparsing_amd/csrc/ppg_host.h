@@ -104,3 +104,58 @@ struct PinnedBuf {
         return hipHostMalloc((void **)&p, std::max<size_t>(count, 1), hipHostMallocDefault);
     }
 };
+
+// DecompressAll state over chunks [first, first+n) of an index (ppg_api.cpp); the cursor and the
+// multi-GPU entry points (ppg_multi.cpp) drive it through the functions below.
+struct ppg_shard {
+    ppg_ctx *ctx = nullptr;
+    int32_t first = 0, n = 0;
+    // compressed file range [Index[first].Input-1, Index[first+n].Input-1]
+    DevBuf<uint8_t> comp_own;
+    const uint8_t *comp = nullptr;
+    int64_t comp_len = 0;
+    uint64_t nwords = 0;
+    DevBuf<PpgInflateJob> jobs;
+    DevBuf<uint8_t> dicts;
+    DevBuf<uint8_t> offs;
+    DevBuf<PpgOffsetRef> oref;
+    DevBuf<PpgInflateResult> res;
+    DevBuf<PpgParseInfo> info;
+    DevBuf<uint64_t> base;     // record base within the batch
+    DevBuf<uint64_t> total;
+    DevBuf<uint8_t> out;
+    DevBuf<uint32_t> recs;
+    DevBuf<uint32_t> nls;      // newline census of the inflate flush (PpgInflateJob::nl_off/nl_cap)
+    int64_t out_cap = 0;
+    std::vector<std::pair<int32_t, int32_t>> batches;   // chunk ranges [b0, b1) relative to first
+    std::vector<PpgInflateJob> h_jobs;
+    // results of the last run
+    std::vector<PpgInflateResult> h_res;
+    std::vector<PpgParseInfo> h_info;
+    std::vector<int64_t> h_base;   // shard-global record base per chunk
+    int64_t total_records = 0;
+    float t_inflate = 0, t_parse = 0, t_total = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t stream = nullptr;   // null: the ctx stream (ppg_file_decompress_all gives each piece shard its own)
+    uint64_t *h_tot = nullptr;      // pinned: a batch's record total, read back without a stream sync
+    int ran = 0;
+    // split chunks (ppg_shard_set_split): the inflate launch runs sub-jobs, ppg_split_merge folds
+    // them back into per-chunk results and census regions
+    int32_t nsub = 0;                            // side points in use (0: one wave per chunk)
+    int64_t base_byte = 0;                       // file byte of comp[0]
+    std::vector<int64_t> h_pout;                 // Output of points first .. first + n
+    std::vector<PpgInflateJob> h_sjobs;
+    DevBuf<PpgInflateJob> sjobs;
+    DevBuf<PpgInflateResult> sres;
+    DevBuf<uint32_t> sidx;                      // chunk k = sub-jobs [sidx[k], sidx[k+1])
+};
+
+int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, const uint8_t *comp, int64_t comp_len,
+                  int64_t out_capacity, hipStream_t s);
+hipStream_t shard_stream(const ppg_shard *sh);
+void shard_reset(ppg_shard *sh);
+int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1);
+int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms);
+int shard_finish(ppg_shard *sh, float total_ms);
+int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n);
+bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads);

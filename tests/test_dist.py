@@ -62,3 +62,39 @@ def test_gather_counts_gloo_world2():
     exp_bases = np.concatenate([[0], np.cumsum(counts_all)[:-1]]).tolist()
     for _, counts, bases in res:
         assert counts == counts_all and bases == exp_bases
+
+
+def test_abi_partition_matches_python_partition():
+    """ppg_partition (the C ABI's) and dist.partition_chunks agree on every golden index."""
+    import parallelparsing_amd as pp
+    from conftest import CASES
+    for name in CASES:
+        meta, gz = load_case(name)
+        ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+        _, inp, _ = ix.arrays()
+        for world in (1, 2, 3, 8):
+            b = pp.partition(ix, world).tolist()
+            assert [(b[r], b[r + 1]) for r in range(world)] == partition_chunks(inp, world), (name, world)
+
+
+def _host_comm_rank(rank, world, name, q):
+    import parallelparsing_amd as pp
+    c = pp.Comm.host(world, rank, name)
+    q.put(c.rank_size())
+    c.close()
+
+
+def test_host_comm_rendezvous_world3():
+    """ppg_comm_init_host: three processes meet in one shared-memory segment (no GPU needed)."""
+    import uuid
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/ppg_cpu_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_host_comm_rank, args=(r, 3, name, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert got == [(0, 3), (1, 3), (2, 3)]

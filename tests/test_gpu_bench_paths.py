@@ -1,0 +1,50 @@
+"""bench.py's multi-rank paths, rehearsed on the one GPU of the box (every rank on cuda:0,
+PPG_BENCH_ONE_DEVICE=1) with gloo for torch.distributed and the library's host transport for the
+count all-gather: the driver's `python bench.py --gpus N` (the bench launches its own ranks) and
+the paired configs[4] path on two ranks, which must find exactly the single-rank pair count."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, ranks=1, timeout=240):
+    env = dict(os.environ, PPG_BENCH_ONE_DEVICE="1", PPG_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    if ranks > 1 and "--gpus" not in args:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+               "--master-addr", "127.0.0.1", "--master-port", str(29400 + os.getpid() % 500)] + cmd[1:]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return lines[0]
+
+
+SMALL = ["--seg-records", "40000", "--repeats", "6", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+         "--no-ingest"]
+
+
+def test_bench_launches_its_own_ranks_and_gathers_in_the_abi():
+    one = _bench(SMALL)
+    two = _bench(SMALL + ["--gpus", "2"])
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["scaling"] == "strong" and two["config"]["workload"].startswith("configs[3]")
+    assert two["config"]["records"] == one["config"]["records"]          # the bench asserts the exact count too
+    assert two["communicator"]["world_size"] == 2
+    assert "ppg_shard_gather_counts" in two["communicator"]["count_gather"]
+
+
+def test_bench_paired_two_ranks_same_pairs():
+    args = ["--paired", "--seg-records", "100000", "--paired-repeats", "3", "--steps", "1", "--warmup", "1"]
+    one = _bench(args)
+    two = _bench(args, ranks=2)
+    assert one["config"]["pairs"] == two["config"]["pairs"] == 300000
+    assert two["n_gpus"] == 2 and two["config"]["pair_check"].startswith("all_to_all")
