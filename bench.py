@@ -47,7 +47,7 @@ def build_input(args):
         # weak (default): ~50 GB of gzip per GPU; strong: one ~50 GB member split over the GPUs
         # (BASELINE configs[3] literally)
         reps = args.repeats * (args.world if args.scaling == "weak" else 1)
-        tf = TiledFile(args.seg_records, reps, args.chunk, threads=args.host_threads)
+        tf = TiledFile(args.seg_records, reps, args.chunk, threads=args.host_threads, blank_lines=args.blank_lines)
     else:  # 1m: configs[1], one non-repeated 1 M-read member
         tf = TiledFile(1_000_000, 1, args.chunk, threads=args.host_threads)
     log(f"[bench] input: {tf.records * tf.repeats:,} records, {tf.text_len * tf.repeats / 1e9:.1f} GB text, "
@@ -450,6 +450,9 @@ def main():
                          "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
                          "0 (default) = auto: enough waves for ~6 generations of the GPU's wave slots (S = 1 for "
                          "the default 50 GB-per-GPU workload, 8 for a strong-scaled rank at N = 8)")
+    ap.add_argument("--blank-lines", action="store_true",
+                    help="side measurement: an empty line after every record, so every chunk takes the declined-chunk "
+                         "parse (ppg_parse_chain; PPG_PARSE_CHAIN=0: the byte-serial lane) -- not the metric's workload")
     ap.add_argument("--no-ingest", action="store_true",
                     help="skip the end-to-end leg (N = 1): DecompressAll straight from the .gz file on disk (host "
                          "ingest, PCIe-inclusive; reported under 'ingest', never as value)")
@@ -596,7 +599,8 @@ def main():
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)",
+        "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)"
+                + (", an empty line after every record (side measurement)" if args.blank_lines else ""),
         "config": {"workload": workload,
                    "records": total_records, "gz_bytes": tf.file_len, "decompressed_bytes": text_bytes,
                    "chunks": nchunks, "parallelism": f"chunk-sharded x{world}",
@@ -618,7 +622,7 @@ def main():
         "reference_published_rec_s": REFERENCE_REC_S,
         "communicator": dict(rccl_info(world, backend), count_gather=gather_via),
     }
-    args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest
+    args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines
     if rank == 0 and world == 1 and (args.ingest or args.create_index):
         del shard, comp
         torch.cuda.empty_cache()

@@ -164,8 +164,8 @@ int ppg_shard_run(ppg_shard *sh);
  * each chunk as one wave per piece between its Point, its side points and the next Point, and
  * fold the pieces back into the chunk (ppg_split_merge): results, records and bytes are
  * identical to the unsplit run.  A side point that is not where the previous piece's blocks end
- * fails the chunk with PPG_DATA_ERROR.  Needs a one-batch shard (else PPG_UNSUPPORTED);
- * nsub = 0 restores one wave per chunk. */
+ * fails the chunk with PPG_DATA_ERROR.  Works with any number of output batches (each batch
+ * launches its chunks' pieces); nsub = 0 restores one wave per chunk. */
 int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
                         const uint8_t *windows);
 

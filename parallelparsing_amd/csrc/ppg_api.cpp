@@ -38,7 +38,7 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
                               int njobs, uint32_t *nls);
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
-                                  PpgParseInfo *info, uint64_t *base, uint64_t *total, int n);
+                                  PpgParseInfo *info, uint64_t *base, uint64_t *total, int n, const uint32_t *nls);
 hipError_t ppg_launch_split_merge(hipStream_t s, const PpgInflateJob *sjobs, const PpgInflateResult *sres,
                                   const uint32_t *sidx, const uint32_t *snls, const PpgInflateJob *jobs,
                                   PpgInflateResult *res, uint32_t *nls, int n);
@@ -495,16 +495,16 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
         horef[(size_t)i].len = (uint32_t)from.offset.size();
         // the offset's own newlines, and whether it alone breaks R-P3 (raw[0] == '\n', "\n\n", NUL)
         uint32_t nl = 0;
-        bool bad = false;
+        bool bad = false, nul = false;
         for (size_t j = 0; j < from.offset.size(); j++) {
             const uint8_t c = from.offset[j];
             if (c == '\n') {
                 nl++;
                 if (j == 0 || from.offset[j - 1] == '\n') bad = true;
             }
-            if (c == 0) bad = true;
+            if (c == 0) bad = nul = true;
         }
-        horef[(size_t)i].nl = nl | (bad ? PPG_OFF_SERIAL : 0u);
+        horef[(size_t)i].nl = nl | (bad ? PPG_OFF_SERIAL : 0u) | (nul ? PPG_OFF_NUL : 0u);
         hoff.insert(hoff.end(), from.offset.begin(), from.offset.end());
     }
     HIPCHK(sh->dicts.alloc((size_t)n * kWin));
@@ -573,19 +573,20 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     hipStream_t s = shard_stream(sh);
     const int nb = b1 - b0;
     HIPCHK(hipEventRecord(sh->ev[0], s));
-    if (sh->nsub) {   // one batch (ppg_shard_set_split checks): sub-jobs, then one result per chunk
+    if (sh->nsub) {   // the batch's sub-jobs, then one result per chunk
+        const uint32_t s0 = sh->h_sidx[(size_t)b0], s1 = sh->h_sidx[(size_t)b1];
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
-                                  sh->sjobs.p, sh->dicts.p, sh->out.p, sh->sres.p, (int)sh->h_sjobs.size(),
+                                  sh->sjobs.p + s0, sh->dicts.p, sh->out.p, sh->sres.p + s0, (int)(s1 - s0),
                                   sh->nls.p));
-        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->sidx.p, sh->nls.p, sh->jobs.p, sh->res.p,
-                                      sh->nls.p, nb));
+        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->sidx.p + b0, sh->nls.p, sh->jobs.p + b0,
+                                      sh->res.p + b0, sh->nls.p, nb));
     } else {
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
                                   sh->jobs.p + b0, sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
     }
     HIPCHK(hipEventRecord(sh->ev[1], s));
     HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
-                                  sh->info.p + b0, sh->base.p + b0, sh->total.p, nb));
+                                  sh->info.p + b0, sh->base.p + b0, sh->total.p, nb, sh->nls.p));
     HIPCHK(hipMemcpyAsync(sh->h_tot, sh->total.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(sh->ev[2], s));
     HIPCHK(ppg_launch_parse_emit(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
@@ -668,7 +669,6 @@ int ppg_shard_run(ppg_shard *sh) {
 int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
                         const uint8_t *windows) {
     if (!sh || nsub < 0 || (nsub && (!bit || !output || !windows))) return PPG_ARG_ERROR;
-    if (nsub && sh->batches.size() != 1) return PPG_UNSUPPORTED;   // sub-jobs need the whole shard resident
     HIPCHK(hipSetDevice(sh->ctx->device));
     hipStream_t s = shard_stream(sh);
     const int32_t n = sh->n;
@@ -695,13 +695,25 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     uint64_t nl_bytes = kNlBytesPerEntry;
     if (const char *e = getenv("PPG_NL_BYTES")) nl_bytes = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     sh->h_sjobs.assign((size_t)n + (size_t)nsub, PpgInflateJob{});
-    // census regions: a chunk left whole keeps its own region of sh->nls (nothing to merge); the
-    // pieces of a split chunk get regions past every chunk's, and the merge copies them back
+    // census regions (batch-relative, like the chunks'): a chunk left whole keeps its own region of
+    // sh->nls (nothing to merge); the pieces of a split chunk get regions past every chunk's of the
+    // same batch, and the merge copies them back
+    std::vector<uint64_t> nl_batch_end((size_t)n, 0);
+    std::vector<uint8_t> batch_first((size_t)n, 0);
+    uint64_t nl_need = 0;
+    for (auto [b0, b1] : sh->batches) {
+        uint64_t e = 0;
+        for (int32_t k = b0; k < b1; k++)
+            e = std::max<uint64_t>(e, sh->h_jobs[(size_t)k].nl_off + sh->h_jobs[(size_t)k].nl_cap);
+        for (int32_t k = b0; k < b1; k++) nl_batch_end[(size_t)k] = e;
+        if (b0 < b1) batch_first[(size_t)b0] = 1;
+        nl_need = std::max(nl_need, e);
+    }
     uint64_t nl_tot = 0;
-    for (int32_t k = 0; k < n; k++)
-        nl_tot = std::max<uint64_t>(nl_tot, sh->h_jobs[(size_t)k].nl_off + sh->h_jobs[(size_t)k].nl_cap);
     int32_t t = 0;
     for (int32_t k = 0; k < n; k++) {
+        if (batch_first[(size_t)k]) nl_tot = nl_batch_end[(size_t)k];   // its pieces' regions: past its chunks'
+
         const PpgInflateJob &C = sh->h_jobs[(size_t)k];
         const int64_t from_out = PO[(size_t)k];
         if (hidx[(size_t)k + 1] - hidx[(size_t)k] == 1) {
@@ -727,6 +739,7 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
             J.nl_off = nl_tot;
             J.nl_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFu);
             nl_tot += J.nl_cap;
+            nl_need = std::max(nl_need, nl_tot);
             sh->h_sjobs[j] = J;
         }
     }
@@ -743,9 +756,10 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     HIPCHK(sh->sres.alloc(sh->h_sjobs.size()));
     HIPCHK(sh->sidx.alloc(hidx.size()));
     HIPCHK(hipMemcpyAsync(sh->sidx.p, hidx.data(), 4 * hidx.size(), hipMemcpyHostToDevice, s));
-    if ((size_t)nl_tot + 64 > sh->nls.n) {   // grow, keeping nothing (the next run rewrites it)
-        HIPCHK(sh->nls.alloc((size_t)nl_tot + 64));
+    if ((size_t)nl_need + 64 > sh->nls.n) {   // grow, keeping nothing (the next run rewrites it)
+        HIPCHK(sh->nls.alloc((size_t)nl_need + 64));
     }
+    sh->h_sidx = hidx;
     HIPCHK(hipStreamSynchronize(s));   // staging vectors and d2 (the old dictionaries) die here
     sh->nsub = nsub;
     return PPG_OK;

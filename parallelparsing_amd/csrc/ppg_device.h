@@ -37,6 +37,7 @@ struct PpgInflateResult {
 
 #define PPG_PF_SERIAL 1     // an empty line (incl. at the offset junction) or a NUL byte in the body
 #define PPG_PF_OVERFLOW 2   // more body newlines than nl_cap: descriptors come from ppg_parse_emit
+#define PPG_PF_NUL 4        // a NUL byte in the body (ppg_parse_chain declines the chunk)
 
 // CreateIndex: one deflate block end (Core.cs:98 -- where inflate(Z_BLOCK) reports data_type & 128)
 struct PpgBlockEnd {
@@ -60,6 +61,8 @@ struct PpgOffsetRef {
 };
 
 #define PPG_OFF_SERIAL 0x80000000u   // offset_k alone has an empty line or a NUL (R-P3)
+#define PPG_OFF_NUL 0x40000000u      // offset_k has a NUL
+#define PPG_OFF_COUNT 0x3FFFFFFFu    // the '\n' count
 
 struct PpgParseInfo {
     uint64_t records;     // FastqRecords emitted by Parsing.Parse for this chunk

@@ -148,6 +148,7 @@ struct ppg_shard {
     DevBuf<PpgInflateJob> sjobs;
     DevBuf<PpgInflateResult> sres;
     DevBuf<uint32_t> sidx;                      // chunk k = sub-jobs [sidx[k], sidx[k+1])
+    std::vector<uint32_t> h_sidx;
 };
 
 int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, const uint8_t *comp, int64_t comp_len,

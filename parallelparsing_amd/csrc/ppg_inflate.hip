@@ -206,11 +206,13 @@ __device__ __forceinline__ void census_step(uint32_t *cen, const CensusOut &co, 
     const uint32_t z = zero_bytes(w0) | zero_bytes(w1) | zero_bytes(w2) | zero_bytes(w3);
     const uint64_t L = __ballot((m >> lastbit) & 1u);   // lanes whose last byte is '\n'
     const uint64_t F = __ballot(m & 1u);                // lanes whose first byte is '\n'
-    const uint64_t B = __ballot((m & (m << 1)) != 0u || z != 0u);
+    const uint64_t B = __ballot((m & (m << 1)) != 0u);
+    const uint64_t Z = __ballot(z != 0u);
     uint32_t cnt = uni(cen[0]);
     const uint32_t prevnl = uni(cen[1]);
     uint32_t flags = uni(cen[2]);
-    if (B | (F & ((L << 1) | prevnl))) flags |= PPG_PF_SERIAL;
+    if (B | Z | (F & ((L << 1) | prevnl))) flags |= PPG_PF_SERIAL;
+    if (Z) flags |= PPG_PF_NUL;
     const uint32_t c = (uint32_t)__builtin_popcount(m);
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t total = rdlane(incl, 63);

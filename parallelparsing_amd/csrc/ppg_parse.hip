@@ -13,6 +13,7 @@
 //                     and one contiguous newline census per chunk, as if one wave had decoded it
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "ppg_device.h"
 
 // ------------------------------------------------------------------------------------------
@@ -35,7 +36,7 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_finish(const PpgInfl
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= nchunks) return;
     const PpgInflateResult r = ires[k];
-    const uint32_t onl = oref[k].nl & ~PPG_OFF_SERIAL;
+    const uint32_t onl = oref[k].nl & PPG_OFF_COUNT;
     const bool ok = r.status == 0;
     const bool serial = (oref[k].nl & PPG_OFF_SERIAL) || (r.pflags & PPG_PF_SERIAL);
     const uint32_t nl = onl + (ok ? r.newlines : 0);
@@ -47,15 +48,26 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_finish(const PpgInfl
     info[k] = f;
 }
 
+// A chunk the census declined (R-P3 fails: an empty line) whose newline positions are all known --
+// the census kept them (no overflow), no NUL byte anywhere, a short offset -- is parsed by
+// ppg_parse_chain from those positions; any other declined chunk byte by byte (ppg_parse_serial).
+constexpr uint32_t kChainOffsetNl = 1024;   // offset newlines ppg_parse_chain stages in LDS
+
+__device__ __forceinline__ bool chain_eligible(const PpgInflateResult &r, const PpgOffsetRef &o, int chain) {
+    return chain && !(r.pflags & (PPG_PF_NUL | PPG_PF_OVERFLOW)) && !(o.nl & PPG_OFF_NUL) &&
+           (o.nl & PPG_OFF_COUNT) <= kChainOffsetNl;
+}
+
 // Parsing.Parse (Parsing.cs:11-69) exactly, one lane per chunk that the census declined.
 // mode 0: count into info[k].records; mode 1: also write descriptors at base[k].
 extern "C" __global__ __launch_bounds__(64) void ppg_parse_serial(
     const uint8_t *__restrict__ out, const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires,
     const uint8_t *__restrict__ offs, const PpgOffsetRef *__restrict__ oref, PpgParseInfo *__restrict__ info,
-    const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks, int mode, uint64_t cap) {
+    const uint64_t *__restrict__ base, uint32_t *__restrict__ recs, int nchunks, int mode, uint64_t cap, int chain) {
     const int k = blockIdx.x;
     if (k >= nchunks || threadIdx.x != 0) return;
     if (!info[k].serial || ires[k].status != 0) return;
+    if (chain_eligible(ires[k], oref[k], chain)) return;   // ppg_parse_chain's
     const uint8_t *body = out + jobs[k].out_off;
     const uint64_t blen = ires[k].produced;
     const uint8_t *off = offs + oref[k].start;
@@ -89,6 +101,99 @@ extern "C" __global__ __launch_bounds__(64) void ppg_parse_serial(
         n++;
     }
     if (!mode) info[k].records = n;
+}
+
+// Parsing.Parse (Parsing.cs:11-69) for a declined chunk from its newline positions, one wave per
+// chunk (replaces the byte-by-byte lane of ppg_parse_serial, which cost a quarter of the inflate
+// time on a file where every chunk has blank lines).  With terminators N[0..M) = the '\n'
+// positions of raw (no NUL: the only 0 is raw[total]), the state machine becomes a walk over
+// terminator indices, O(1) per record: a record starting after the previous record's n4 = N[p]
+//   n1 = the first '\n' at or after N[p] + 2   (raw[N[p]+1] was skipped as the '@', Parsing.cs:19)
+//      = N[p+1], or N[p+2] if N[p+1] == N[p] + 1 (a blank line there)
+//   n2 = the next '\n' = N[j1+1]
+//   n3 = the first '\n' at or after n2 + 2     (raw[n2+1] skipped as the '+', Parsing.cs:30)
+//   n4 = the next '\n'
+// and any terminator index >= M is the 0 at raw[total] (ParseLine's stop: no record).  The walk
+// is wave-uniform; the terminators come 64 at a time into a VGPR window read with v_readlane, and
+// descriptors leave 16 records (64 dwords) per vector store.
+extern "C" __global__ __launch_bounds__(64) void ppg_parse_chain(
+    const PpgInflateJob *__restrict__ jobs, const PpgInflateResult *__restrict__ ires, const uint8_t *__restrict__ offs,
+    const PpgOffsetRef *__restrict__ oref, PpgParseInfo *__restrict__ info, const uint64_t *__restrict__ base,
+    const uint32_t *__restrict__ nls, uint32_t *__restrict__ recs, int nchunks, int mode, uint64_t cap) {
+    __shared__ uint32_t onl_pos[kChainOffsetNl];
+    const int k = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    if (k >= nchunks) return;
+    const PpgInflateResult r = ires[k];
+    const PpgOffsetRef o = oref[k];
+    if (!info[k].serial || r.status != 0 || !chain_eligible(r, o, 1)) return;
+    // the offset's newlines (raw indices [0, olen)), in order
+    const uint8_t *off = offs + o.start;
+    const uint32_t olen = o.len;
+    uint32_t onl = 0;
+    for (uint32_t g = 0; g < olen; g += 64) {
+        const bool nl = g + lane < olen && off[g + lane] == '\n';
+        const uint64_t b = __ballot(nl);
+        if (nl) onl_pos[onl + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = g + lane;
+        onl += (uint32_t)__popcll(b);
+    }
+    __syncthreads();
+    const int64_t M = (int64_t)onl + r.newlines;
+    const uint64_t total = (uint64_t)olen + r.produced;
+    const uint32_t *bnl = nls + jobs[k].nl_off;
+    auto load = [&](int64_t wb) -> uint32_t {
+        const int64_t j = wb + (int64_t)lane;
+        return j < (int64_t)onl ? onl_pos[j] : (j < M ? bnl[j - onl] : 0u);
+    };
+    int64_t wb = 0;
+    uint32_t win = load(0);
+    auto N = [&](int64_t j) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(j - wb)); };
+    uint64_t count = 0;
+    const uint64_t b0 = mode ? base[k] : 0;
+    uint32_t acc = 0;                                  // lane 4q+f: field f of the q-th pending record
+    int64_t p = -1;
+    uint64_t np1 = 0;                                  // N[p] + 1: where the next record's state starts
+    for (;;) {
+        if (np1 >= total) break;                       // raw[i] == 0 (Parsing.cs:16)
+        if (p + 7 > wb + 64) {                         // indices up to p + 6 must be in the window
+            wb = p + 1;
+            win = load(wb);
+        }
+        int64_t j = p + 1;
+        if (j >= M) break;
+        uint32_t n1 = N(j);
+        if (n1 == np1) {                               // raw[N[p]+1] == '\n': skipped, then a blank line
+            if (++j >= M) break;
+            n1 = N(j);
+        }
+        if (++j >= M) break;
+        const uint32_t n2 = N(j);
+        if (++j >= M) break;
+        uint32_t n3 = N(j);
+        if (n3 == n2 + 1) {                            // the skipped '+' byte was a '\n'
+            if (++j >= M) break;
+            n3 = N(j);
+        }
+        if (++j >= M) break;
+        const uint32_t n4 = N(j);
+        if (mode) {
+            const uint32_t q = (uint32_t)(count & 15) * 4;
+            acc = lane == q ? n1 : lane == q + 1 ? n2 : lane == q + 2 ? n3 : lane == q + 3 ? n4 : acc;
+            if ((count & 15) == 15) {                  // 16 records: one 256-B store
+                const uint64_t at = 4 * (b0 + count - 15) + lane;
+                if (4 * (b0 + count + 1) <= cap) recs[at] = acc;
+            }
+        }
+        count++;
+        p = j;
+        np1 = (uint64_t)n4 + 1;
+    }
+    if (mode) {
+        const uint32_t q = (uint32_t)(count & 15);
+        if (q && lane < 4 * q && 4 * (b0 + count) <= cap) recs[4 * (b0 + count - q) + lane] = acc;
+    } else if (lane == 0) {
+        info[k].records = count;
+    }
 }
 
 // Exclusive scan of info[].records -> base[] and total (single workgroup; chunks <= a few 1e5).
@@ -197,7 +302,7 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_place(
     if (4 * (base[k] + f.records) > cap) return;   // the host grows the buffer and runs this again
     const uint64_t limit = 4 * f.records;
     uint32_t *dst = recs + 4 * base[k];
-    const uint32_t onl = oref[k].nl & ~PPG_OFF_SERIAL;
+    const uint32_t onl = oref[k].nl & PPG_OFF_COUNT;
     if (onl && threadIdx.x == 0) {
         const uint8_t *off = offs + oref[k].start;
         uint64_t m = 0;
@@ -353,13 +458,23 @@ extern "C" __global__ __launch_bounds__(256) void ppg_split_merge(const PpgInfla
 // Host-side launchers (called from ppg_api.cpp).
 // ------------------------------------------------------------------------------------------
 // after the inflate launch: per-chunk counts (census, or the serial machine) and their scan
+// PPG_PARSE_CHAIN=0 parses every declined chunk byte by byte (A/B and tests of both paths)
+static int chain_enabled() {
+    const char *e = getenv("PPG_PARSE_CHAIN");
+    return e && e[0] == '0' ? 0 : 1;
+}
+
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
-                                  PpgParseInfo *info, uint64_t *base, uint64_t *total, int n) {
+                                  PpgParseInfo *info, uint64_t *base, uint64_t *total, int n, const uint32_t *nls) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(ppg_parse_finish, dim3((n + 255) / 256), dim3(256), 0, s, ires, oref, info, n);
+    const int chain = chain_enabled();
     hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info,
-                       (const uint64_t *)nullptr, (uint32_t *)nullptr, n, 0, (uint64_t)0);
+                       (const uint64_t *)nullptr, (uint32_t *)nullptr, n, 0, (uint64_t)0, chain);
+    if (chain)
+        hipLaunchKernelGGL(ppg_parse_chain, dim3(n), dim3(64), 0, s, jobs, ires, offs, oref, info,
+                           (const uint64_t *)nullptr, nls, (uint32_t *)nullptr, n, 0, (uint64_t)0);
     hipLaunchKernelGGL(ppg_scan_counts, dim3(1), dim3(1024), 0, s, info, base, total, n);
     return hipGetLastError();
 }
@@ -372,7 +487,12 @@ hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInf
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(ppg_parse_place, dim3(n), dim3(256), 0, s, jobs, ires, offs, oref, info, base, nls, recs, n, cap);
     hipLaunchKernelGGL(ppg_parse_emit, dim3(n), dim3(256), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, cap);
-    hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, 1, cap);
+    const int chain = chain_enabled();
+    hipLaunchKernelGGL(ppg_parse_serial, dim3(n), dim3(64), 0, s, out, jobs, ires, offs, oref, info, base, recs, n, 1, cap,
+                       chain);
+    if (chain)
+        hipLaunchKernelGGL(ppg_parse_chain, dim3(n), dim3(64), 0, s, jobs, ires, offs, oref, info, base, nls, recs, n, 1,
+                           cap);
     return hipGetLastError();
 }
 

@@ -17,13 +17,21 @@ from . import Index
 
 class TiledFile:
     def __init__(self, records, repeats, chunksize, read_len=150, seed=0, level=6, piece=4 << 20, threads=16,
-                 mate=0):
+                 mate=0, blank_lines=False):
         S = synth()
         self.records, self.repeats, self.chunksize = records, repeats, chunksize
+        self.blank_lines = blank_lines
         n = S.ppg_synth_fastq_size_mate(0, records, read_len, mate)
         self.text = np.empty(n, np.uint8)
         assert S.ppg_synth_fastq_mate(seed, mate, 0, records, read_len, C.c_void_p(self.text.ctypes.data), n,
                                       threads) == n
+        if blank_lines:
+            # an empty line after every record: every chunk fails R-P3 and takes the
+            # declined-chunk parse (ppg_parse_chain); each record still parses, its Identifier
+            # starting with the '@' (the blank line is what Parsing.cs:19 skips)
+            ends = np.nonzero(self.text == 10)[0][3::4] + 1
+            self.text = np.insert(self.text, ends, np.uint8(10))
+            n = self.text.size
         cap = n // 2 + (1 << 20)
         seg = np.empty(cap, np.uint8)
         crc = C.c_uint32()
@@ -70,7 +78,7 @@ class TiledFile:
             a = int(self._p_at[p]) % tl
             n = int(self.p_offlen[p])
             seg = self.text[a:a + n] if a + n <= tl else np.concatenate([self.text[a:], self.text[:a + n - tl]])
-            dup += int(np.count_nonzero(seg == 10) == 4)
+            dup += int(np.count_nonzero(seg == 10) == (5 if self.blank_lines else 4))
         return self.records * self.repeats + dup
 
     def windows(self, lo=0, hi=None):

@@ -332,8 +332,23 @@ def test_split_rejects_bad_side_points(device):
         sh.run()
     r = sh.results()
     assert (r["status"] != 0).sum() == 1
-    # batched shards cannot be split
-    b = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device, out_capacity=8192)
-    if b.batches > 1:
-        with pytest.raises(RuntimeError):
-            b.set_split(bits, outs, win)
+
+
+@pytest.mark.parametrize("name,cap", [("memlevel1_c10", 8192), ("l6_c200", 200000), ("crlf_c100", 100000),
+                                      ("fixed_c100", 60000)])
+def test_split_multi_batch_shards(name, cap, device):
+    """a shard whose output does not fit one batch can still be split; each batch
+    launches its chunks' pieces and the results equal the unsplit, one-batch run."""
+    meta, gz = load_case(name)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    n = ix.Count - 1
+    bits, outs, win = dense_side_points(gz, ix)
+    one = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device, out_capacity=cap)
+    assert sh.batches > 2
+    sh.set_split(bits, outs, win).run()
+    ra, rb = one.results(), sh.results()
+    for key in ra:
+        assert (ra[key] == rb[key]).all(), key
+    assert sh.total_records == meta["total_records"]
+    assert (sh.record_base() == one.record_base()).all()

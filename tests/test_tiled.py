@@ -79,3 +79,17 @@ def test_side_points_of_a_range_match_the_whole():
     keep = (o_all > tf.p_output[lo]) & (o_all < tf.p_output[hi - 1])
     assert np.array_equal(o, o_all[keep]) and np.array_equal(b, b_all[keep])
     assert w.tobytes() == w_all.reshape(-1, 32768)[keep].tobytes()
+
+
+@pytest.mark.parametrize("records,repeats,chunk", [(3000, 4, 500), (2000, 3, 40)])
+def test_blank_line_member_points_and_count(records, repeats, chunk):
+    """bench.py --blank-lines (every chunk takes the declined-chunk parse): the member's derived
+    Points equal the oracle's CreateIndex, and DecompressAll's count equals expected_records."""
+    tf = TiledFile(records, repeats, chunk, threads=4, blank_lines=True)
+    assert tf.text.tobytes().count(b"\n\n") == records
+    f = tf.file_bytes().tobytes()
+    assert gzip.decompress(f) == tf.text.tobytes() * repeats
+    oi = O.build_index(f, chunk)
+    assert [p[:3] for p in oi.points()] == list(zip(tf.p_output.tolist(), tf.p_input.tolist(), tf.p_bits.tolist()))
+    tot, _ = O.decompress_all(f, oi, threads=4)
+    assert tot == tf.expected_records()
