@@ -151,3 +151,77 @@ def test_record_keys_drop_q1_duplicates(tmp_path):
     assert bits.size >= n // 2
     s2 = pp.Shard(ix, np.frombuffer(gz[i0 - 1:i1], np.uint8), 0, n).set_split(bits, outs, win).run()
     assert torch.equal(paired.shard_keys(s2), keys)
+
+
+def _ref_keys(raw, desc, olen):
+    """ppg_record_keys' byte loop (ppg_parse.hip), restated for the test: the digits between the
+    Identifier's first two '.', at most 18 of them, within its first 96 bytes; -2 for a chunk's
+    first record lying wholly inside offset_k (parsed twice)."""
+    out = []
+    for j, (n1, n2, n3, n4) in enumerate(desc.tolist()):
+        start = 0 if j == 0 else desc[j - 1][3] + 1
+        if j == 0 and n4 < olen:
+            out.append(-2)
+            continue
+        end = min(n1, start + 96)
+        i, key = start + 1, -1
+        while i < end and raw[i] != ord("."):
+            i += 1
+        if i < end:
+            i += 1
+            v = nd = c = 0
+            while i < end:
+                c = raw[i]
+                if not (48 <= c <= 57 and nd < 18):
+                    break
+                v, nd, i = v * 10 + c - 48, nd + 1, i + 1
+            if nd > 0 and i < end and c == ord("."):
+                key = v
+        out.append(key)
+    return out
+
+
+HEADERS = [
+    b"@SRR1.{n}.1 {n} length=8",                          # the ordinary shape
+    b"@" + b"A" * 60 + b".{n}.2 tail",                    # first '.' past the 48-byte window
+    b"@X" + b"B" * 100 + b".{n}.1",                       # past the 96-byte bound: -1
+    b"@SRR.123456789012345678.1",                         # 18 digits
+    b"@SRR.1234567890123456789.1",                        # 19 digits: -1
+    b"@SRR.{n} no second dot",                            # -1
+    b"@SRR..1",                                           # empty spot: -1
+    b"@SRR.{n}",                                          # the line ends inside the digits: -1
+    b"@" + b"C" * 31 + b".{n}.",                          # identifier of 48 bytes-ish, decided at the end
+    b"@" + b"D" * 38 + b".12345678.",                     # exactly 48 bytes after the '@'
+    b"@.{n}.x",                                           # the first byte is the '.'
+    b"@noDots",
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [7, 23])
+def test_record_keys_identifier_edge_cases(chunk, device):
+    """ppg_record_keys' 48-byte register window and its byte-loop fallback against the
+    byte loop restated in Python, on identifiers that reach every branch, with headers straddling
+    Points (small chunks, Huffman-only: Points land on record starts too, giving Q1 duplicates)."""
+    import zlib
+    recs = []
+    for i in range(600):
+        h = HEADERS[i % len(HEADERS)].replace(b"{n}", str(1000 + i).encode())
+        recs.append(h + b"\nACGTACGT\n+\n????????\n")
+    text = b"".join(recs)
+    c = zlib.compressobj(6, zlib.DEFLATED, 31, 8, zlib.Z_HUFFMAN_ONLY)
+    gz = c.compress(text) + c.flush()
+    ix = pp.Core.BuildDeflateIndex(gz, chunk)
+    n = ix.Count - 1
+    _, i0, _, _ = ix.point_fields(0)
+    _, i1, _, _ = ix.point_fields(n)
+    sh = pp.Shard(ix, np.frombuffer(gz[i0 - 1:i1], np.uint8), 0, n, device=device).run()
+    got = paired.shard_keys(sh).cpu().numpy().tolist()
+    exp = []
+    for k in range(n):
+        off = ix[k].offset
+        raw = off + sh.chunk_bytes(k).tobytes()
+        exp += _ref_keys(raw, sh.chunk_records(k), len(off))
+    assert got == exp
+    assert exp.count(-2) > 0 and exp.count(-1) > 100 and 123456789012345678 in exp
+    assert {1000 + i for i in range(0, 600, len(HEADERS))} <= set(exp)   # ordinary keys decoded

@@ -9,8 +9,11 @@ between ;;#ASMSTART and ;;#ASMEND, checks the instructions before it:
   * global_load_lds_* reads M0: 1 wait state after a SALU write, 5 after a VALU write;
   * v_readlane / v_writelane with an SGPR or M0 lane select: 4 wait states after a VALU write.
 
-A plain instruction counts one wait state, s_nop N counts N + 1.  The scan runs backwards in
-program order across labels (the fall-through predecessor).  Exit status 1 lists the violations.
+A plain instruction counts one wait state, s_nop N counts N + 1.  The scan runs backwards over
+every predecessor path: at a label it follows both the fall-through predecessor (unless that is an
+unconditional s_branch) and every branch that jumps to the label (s_branch / s_cbranch_*, named
+.LBB labels and the asm's numeric local labels "1b"/"1f"), and takes the fewest wait states over
+all paths.  Exit status 1 lists the violations.
 (Found with amdgpu_num_sgpr(64): a spilled far-load base restored right before the load faulted.)
 
   python tools/hazard_lint.py file.s [kernel-name-substring]
@@ -35,11 +38,18 @@ def sregs(tok):
 
 def parse(line):
     s = line.split(";")[0].strip()
-    if not s or s.endswith(":") or s.startswith("."):
+    if not s or s.startswith("."):
+        if s.startswith(".L") and s.endswith(":"):
+            return ("label", s[:-1])
         return None
+    if s.endswith(":"):
+        return ("label", s[:-1])
     parts = s.split(None, 1)
     ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
     return parts[0], ops
+
+
+BRANCH = re.compile(r"s_(branch|cbranch_\w+)$")
 
 
 def writes(mn, ops):
@@ -74,9 +84,8 @@ def needs(mn, ops):
 
 
 def lint(lines, kernel=None):
-    bad = []
     in_kernel = kernel is None
-    insts = []          # (index in file, mnemonic, ops, in_asm)
+    insts = []          # (index in file, mnemonic or "label", ops or label name, in_asm)
     in_asm = False
     for i, line in enumerate(lines):
         if kernel is not None and re.match(r"^[_A-Za-z0-9.$]+:", line):
@@ -94,25 +103,71 @@ def lint(lines, kernel=None):
         p = parse(line)
         if p:
             insts.append((i, p[0], p[1], in_asm))
+    # branch sources of every label position: named labels anywhere, numeric local labels
+    # ("1:" referenced as "1b" / "1f") resolved to the nearest one before / after the branch
+    labels = {}
+    numeric = {}
+    for k, (_, mn, op, _) in enumerate(insts):
+        if mn == "label":
+            labels.setdefault(op, k)
+            if op.isdigit():
+                numeric.setdefault(op, []).append(k)
+    preds = {}
+    for k, (_, mn, ops, _) in enumerate(insts):
+        if mn == "label" or not BRANCH.match(mn) or not ops:
+            continue
+        tgt = ops[-1]
+        m = re.fullmatch(r"(\d+)([bf])", tgt)
+        if m:
+            cands = numeric.get(m.group(1), [])
+            before = [c for c in cands if c < k]
+            after = [c for c in cands if c > k]
+            t = (before[-1] if before else None) if m.group(2) == "b" else (after[0] if after else None)
+        else:
+            t = labels.get(tgt)
+        if t is not None:
+            preds.setdefault(t, []).append(k)
+
+    def fewest(k, regs, need_v, need_s, ws, seen):
+        """(wait states, writer index) on the worst path back from instruction k, or None."""
+        worst = None
+        j = k - 1
+        while j >= 0:
+            _, mj, oj, _ = insts[j]
+            if mj == "label":
+                for src in preds.get(j, []):
+                    if (src, ws) in seen:
+                        continue
+                    seen.add((src, ws))
+                    r = fewest(src + 1, regs, need_v, need_s, ws, seen)   # the branch itself is the predecessor
+                    if r and (worst is None or r[0] < worst[0]):
+                        worst = r
+                prev = insts[j - 1][1] if j > 0 else None
+                if prev == "s_branch":
+                    return worst
+                j -= 1
+                continue
+            kind, w = writes(mj, oj)
+            if w & regs:
+                need = need_v if kind == "valu" else need_s
+                if ws < need and (worst is None or ws < worst[0]):
+                    worst = (ws, j, need)
+                return worst
+            ws += (int(oj[0], 0) + 1 if oj else 1) if mj == "s_nop" else 1
+            if ws >= 5:
+                return worst
+            j -= 1
+        return worst
+
+    bad = []
     for k, (i, mn, ops, asm) in enumerate(insts):
-        if not asm:
+        if not asm or mn == "label":
             continue
         for regs, need_v, need_s in needs(mn, ops):
-            ws = 0
-            for j in range(k - 1, max(-1, k - 12), -1):
-                _, mj, oj, _ = insts[j]
-                kind, w = writes(mj, oj)
-                if w & regs:
-                    need = need_v if kind == "valu" else need_s
-                    if ws < need:
-                        bad.append((i + 1, mn, " ".join(ops), insts[j][0] + 1, mj, ws, need))
-                    break
-                if mj == "s_nop":
-                    ws += int(oj[0], 0) + 1 if oj else 1
-                else:
-                    ws += 1
-                if ws >= 5:
-                    break
+            r = fewest(k, regs, need_v, need_s, 0, set())
+            if r:
+                ws, j, need = r
+                bad.append((i + 1, mn, " ".join(ops), insts[j][0] + 1, insts[j][1], ws, need))
     return bad
 
 
