@@ -574,7 +574,8 @@ def main():
     else:
         total_records = local_records
     expect = tf.expected_records()   # includes the reference's Q1 duplicates
-    assert total_records == expect, (total_records, expect)
+    if not os.environ.get("PPG_PROBE_NO_CENSUS"):   # an A/B timing probe produces no records
+        assert total_records == expect, (total_records, expect)
 
     text_bytes = int(ix_out[-1] - ix_out[0])
     comp_total = int(ix_in[-1] - ix_in[0])

@@ -25,6 +25,7 @@
 //     from HBM; completed 4 KiB units leave the ring as 16-B-per-lane coalesced stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 
@@ -889,6 +890,10 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
                               int njobs, uint32_t *nls) {
     if (njobs <= 0) return hipSuccess;
+    // A/B probe only (PPG_PROBE_NO_CENSUS=1): the kernel without the fused newline census, to time
+    // what the census costs; the records of such a run are not valid
+    static const bool no_census = getenv("PPG_PROBE_NO_CENSUS") != nullptr;
+    if (no_census) nls = nullptr;
 #define X(R, L)                                                                                               \
     if (ring_bits == R && lit_bits == L) {                                                                    \
         if (nls)                                                                                              \
