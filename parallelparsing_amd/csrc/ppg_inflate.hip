@@ -33,6 +33,35 @@
 // last 32 KiB + REACH are ever read back)
 #define IX_RING_BYTES 65536u
 #define IX_RING_MASK (IX_RING_BYTES - 1u)
+#define PPG_STR2(x) #x
+#define PPG_STR(x) PPG_STR2(x)
+// Wave priority (s_setprio) by phase of the token round: the decode (PPG_DEC_PRIO, default none =
+// 0), the serial walk (PPG_WALK_PRIO) and after it until the round's bytes are written
+// (PPG_EMIT_PRIO), held through the round's tail (PPG_TAIL_PRIO: pos/carry/flush) and dropped to 0
+// before the next round's decode.  A wave that has walked its round finishes it ahead of waves
+// still decoding theirs: the walk and the emit are one serial chain of dependent LDS / lane /
+// far-load latencies, the decode is VALU-dense and latency-tolerant.  Measured on the 50 GB step
+// (tools/ab_bench.sh, r02): none 840.4 ms; walk 2: 815-818; walk 2 + emit 1: 794.7; + tail: 793.3;
+// walk 1 + emit 1: 795.2; decode 1 as well: 846.4 (priority on the decode costs what it gains).
+// PPG_NO_PRIO builds the kernel without any of it.
+#ifndef PPG_NO_PRIO
+#ifndef PPG_WALK_PRIO
+#define PPG_WALK_PRIO 2
+#endif
+#ifndef PPG_EMIT_PRIO
+#define PPG_EMIT_PRIO 1
+#endif
+#ifndef PPG_TAIL_PRIO
+#define PPG_TAIL_PRIO 1
+#endif
+#endif
+#ifndef PPG_POST_WALK_PRIO
+#ifdef PPG_EMIT_PRIO
+#define PPG_POST_WALK_PRIO PPG_EMIT_PRIO
+#else
+#define PPG_POST_WALK_PRIO 0
+#endif
+#endif
 
 template <int RB, int LBT>
 struct __attribute__((aligned(16))) InflateLds {
@@ -387,6 +416,7 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 // v_writelane (at output offset (X >> 8)[5:0]), one s_add, and s_and's SCC as the loop test —
 // written out because the compiler adds an s_cmp_eq 0 after the s_and (one more SALU per token,
 // and SALU issue is what bounds this kernel).  The order is the compiler's own hazard-clean one.
+template <uint32_t STOPMASK = 0x1C0C0u>
 __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
     uint32_t t, tmp;
     asm volatile(
@@ -394,11 +424,11 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
         "v_readlane_b32 %[t], %[vt], %[X]\n\t"
         "s_lshr_b32 m0, %[X], 8\n\t"
         "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "s_and_b32 %[tmp], %[X], %[M]\n\t"
         "v_writelane_b32 %[vtin], %[t], m0\n\t"
         "s_cbranch_scc0 1b"
         : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
-        : [vt] "v"(vt)
+        : [vt] "v"(vt), [M] "i"(STOPMASK)
         : "m0", "scc");
 }
 
@@ -632,6 +662,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
             bool spec = false;
             if (off < min(64u, len - pos)) {
+#ifdef PPG_DEC_PRIO
+                asm volatile("s_setprio " PPG_STR(PPG_DEC_PRIO));
+#endif
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring; st_enter already made the segment resident)
                 const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
@@ -657,28 +690,49 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 uint32_t X;
                 if (len - pos >= 64) {
                     X = off << 8;
-#ifdef PPG_WALK_C
+#ifdef PPG_WALK_PRIO
+                    asm volatile("s_setprio " PPG_STR(PPG_WALK_PRIO));
+#endif
+#if defined(PPG_WALK_C)
                     do {
                         t = rdlane(vta, X);
                         vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
                         X += t;
                     } while ((X & STOP) == 0u);
-#else
-                    walk_asm(vta, vtin, X);
-#endif
                     if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
                         X -= 64;
                         half = 64;
-#ifdef PPG_WALK_C
                         do {
                             t = rdlane(vtb, X);
                             vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
                             X += t;
                         } while ((X & STOP) == 0u);
-#else
-                        walk_asm(vtb, vtin, X);
-#endif
                     }
+#elif defined(PPG_WALK_CONT)
+                    // s runs on through the second span (v_readlane uses s[5:0] = s - 64 there):
+                    // that walk stops at s >= 128 (bit 7) or off >= 64; a special token in it
+                    // leaves s >= 192, one in the first span s in [128, 192) -- no rebasing
+                    walk_asm(vta, vtin, X);
+                    if ((X & (STOP & ~0x40u)) == 0u) {
+                        walk_asm<0x1C080u>(vtb, vtin, X);
+                        const bool sp2 = (X & 0xC0u) == 0xC0u;
+                        off = (X >> 8) & 511u;
+#ifdef PPG_WALK_PRIO
+                        asm volatile("s_setprio " PPG_STR(PPG_POST_WALK_PRIO));
+#endif
+                        return Round{vtin, off, (X & 255u) - (sp2 ? 128u : 0u), sp2};
+                    }
+#else
+                    walk_asm(vta, vtin, X);
+                    if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
+                        X -= 64;
+                        half = 64;
+                        walk_asm(vtb, vtin, X);
+                    }
+#endif
+#ifdef PPG_WALK_PRIO
+                    asm volatile("s_setprio " PPG_STR(PPG_POST_WALK_PRIO));
+#endif
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -781,6 +835,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 }
 #endif
                 S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
+#if (defined(PPG_DEC_PRIO) || defined(PPG_EMIT_PRIO)) && !defined(PPG_TAIL_PRIO)
+                asm volatile("s_setprio 0");
+#endif
             }
             cn = tot - rout;
             if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
@@ -793,6 +850,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 fl_next += UNIT;
             }
             bp += R.adv;
+#ifdef PPG_TAIL_PRIO
+            asm volatile("s_setprio 0");
+#endif
             if constexpr (IX) {   // past the member, or runaway output (a false start)
                 if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
             }
