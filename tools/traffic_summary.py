@@ -3,11 +3,13 @@
   python tools/traffic_summary.py <tag>
 writes profiles/<tag>_bench_kernel_stats.csv (rocprofv3 --stats, copied), profiles/<tag>_bench.json
 (the bench line of the profiled run) and profiles/traffic.json (HBM bytes per inflate launch, read
-by bench.py for roofline.traffic).  Counter conventions (MI355X_MICROARCH.md, HBM section):
-FETCH_SIZE is doubled for the parse/copy kernels' 16-B-per-lane streaming reads; the inflate
-kernel's reads (4-B LDS-DMA stream words, 4-B far back-reference loads, 32 KiB windows) are an
-uncalibrated width and are taken as reported.  WRITE_SIZE is taken as reported.  rocprofv3
-reports both in KiB."""
+by bench.py for roofline.traffic).  Counter conventions (MI355X_MICROARCH.md, HBM section, and
+tools/fetch_calib.hip, profiles/r02_fetch_calib.json): on gfx950 FETCH_SIZE tallies 64 B per
+128-B memory-side request for every read shape the inflate kernel uses -- a coalesced 4-B-per-lane
+read of B bytes reports B/2 (as the guide's 16-B-per-lane case), and a 4-B read landing in its own
+128-B line reports 64 B -- so FETCH_SIZE is doubled for every kernel.  WRITE_SIZE is taken as
+reported.  rocprofv3 reports both in KiB.  Infinity-Cache hits are counted too: the figure is
+memory-side traffic out of the L2s, an upper bound on HBM bytes."""
 import csv
 import glob
 import json
@@ -49,17 +51,19 @@ def main(tag):
     out = {
         "workload": b["config"]["workload"],
         "command": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) -- "
-                   "python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline",
+                   "python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest",
         "kernel": short(inf),
         "launches": n,
-        "fetch_bytes": fetch[inf] / n,
+        "fetch_size_reported_bytes": fetch[inf] / n,
+        "fetch_bytes": 2 * fetch[inf] / n,
         "write_bytes": write.get(inf, 0.0) / n,
-        "hbm_bytes_per_launch": (fetch[inf] + write.get(inf, 0.0)) / n,
+        "hbm_bytes_per_launch": (2 * fetch[inf] + write.get(inf, 0.0)) / n,
         "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
-        "note": "FETCH_SIZE (L2 memory-side requests, Infinity-Cache hits included) taken as reported for the "
-                "inflate kernel: its reads are 4 B per lane (LDS-DMA stream words, far back-references, windows), "
-                "not the 16-B/lane streaming pattern the guide's x2 gfx950 correction is calibrated for. "
-                "WRITE_SIZE covers the decompressed bytes and the census's stored newline positions.",
+        "note": "fetch_bytes = 2 x FETCH_SIZE: calibrated on gfx950 for the inflate kernel's own read shapes "
+                "(tools/fetch_calib.hip, profiles/r02_fetch_calib.json: coalesced 4-B-per-lane and scattered 4-B "
+                "reads both tally 64 B per 128-B request).  Memory-side traffic out of the L2s, Infinity-Cache hits "
+                "included (an upper bound on HBM bytes).  WRITE_SIZE covers the decompressed bytes and the census's "
+                "stored newline positions.",
         "other_kernels": {short(k): {"fetch_bytes_x2": 2 * v, "write_bytes": write.get(k, 0.0)}
                           for k, v in fetch.items() if k != inf and "ppg_" in k},
     }
