@@ -112,7 +112,11 @@ struct Reader {
 // only by st_enter's explicit s_waitcnt; an untracked VMEM op can only make the compiler's own
 // vmcnt waits stricter, never looser.  (s_nop: SALU write of M0 -> LDS DMA needs one wait state.)
 __device__ __forceinline__ void lds_dma_dword(const uint32_t *src, const uint32_t *lds_base) {
+#ifdef PPG_STREAM_NT
+    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)lds_base)
+#else
     asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)lds_base)
+#endif
                  : "memory");
 }
 
@@ -253,7 +257,11 @@ __device__ __forceinline__ void census_step(uint32_t *cen, const CensusOut &co, 
             if (mm) {
                 const uint32_t b = (uint32_t)__builtin_ctz(mm);
                 mm &= mm - 1u;
+#ifdef PPG_CENSUS_NT
+                if (idx < co.cap) __builtin_nontemporal_store(co.shift + p_lane + b, co.dst + idx);
+#else
                 if (idx < co.cap) ((__attribute__((address_space(1))) uint32_t *)co.dst)[idx] = co.shift + p_lane + b;
+#endif
                 idx++;
             }
         }
@@ -339,6 +347,18 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, con
 __device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) {
     uint32_t v;
     asm volatile("global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+    return v;
+}
+
+// far_load in two halves (PPG_FAR_SPLIT): the load, and the wait that hands its result over.  The
+// value is an in/out operand of the wait, so nothing reads it before the load has landed.
+__device__ __forceinline__ uint32_t far_issue(const uint8_t *base, uint32_t off) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, %2" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint32_t far_wait(uint32_t v) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : : "memory");
     return v;
 }
 
@@ -780,21 +800,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
                 const uint32_t inf = bperm(sj << 2, R.vtin);
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
+#ifdef PPG_FAR_SPLIT
+                // the far load goes out before the ring read, so the two latencies overlap
+                const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
+                const uint64_t fm = __ballot(far);
+                const int32_t fp = (int32_t)pos + jj;
+                const uint32_t fq = (oa + (uint32_t)fp) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
+                uint32_t fw = 0;
+                if (fm) fw = far_issue(ob, far && fp >= 0 ? (fq & ~3u) : 0u);
+                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+#else
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
                 const uint64_t fm = __ballot(far);
+#endif
 #ifdef PPG_STATS
                 if (fm) st_far++;
 #endif
+#ifdef PPG_PROBE_NO_FAR
+                if (false) {   // timing probe only: far bytes read from the ring (wrong output)
+#else
                 if (fm) {
+#endif
                     // older than the ring: the flushed output (this wave's own earlier stores), as
                     // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
                     // juggling); references into the Point's window (first 32 KiB only) separately
+#ifdef PPG_FAR_SPLIT
+                    const int32_t p = fp;
+                    const uint32_t q = fq;
+                    const bool fo = far && p >= 0;
+                    const uint32_t w = far_wait(fw);
+#else
                     const int32_t p = (int32_t)pos + jj;
                     const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
                     const bool fo = far && p >= 0;
                     const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
+#endif
                     val = fo ? (w >> (8 * (q & 3))) & 255u : val;
                     const bool fd = far && p < 0;
                     const uint64_t dm = __ballot(fd);
@@ -845,6 +888,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             }
             pos += rout;
             if (pos >= fl_next) {
+#ifdef PPG_FLUSH_PRIO
+                asm volatile("s_setprio " PPG_STR(PPG_FLUSH_PRIO));
+#endif
                 flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
