@@ -461,7 +461,12 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
 #define PPG_NUM_SGPR 80
 #endif
 template <int RB, int LBT, bool IX, bool CEN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
+#ifdef PPG_NUM_VGPR
+#define PPG_VGPR_ATTR __attribute__((amdgpu_num_vgpr(PPG_NUM_VGPR), amdgpu_waves_per_eu(8, 8)))
+#else
+#define PPG_VGPR_ATTR
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) PPG_VGPR_ATTR void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
