@@ -31,6 +31,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+SEG_RECORDS = 10_485_760     # default 50 GB workload: a ~4 GB-text segment ...
+REPEATS = 51                 # ... repeated 51 times in one member (~50 GB of gzip)
+PAIRED_SEG_RECORDS = 2_621_440
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 REFERENCE_REC_S = 1.217e6  # Plots/csv_original/parallel_10k_false.csv:8 (Arm64, published; not this metric)
 
@@ -428,8 +431,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="50gb", choices=["50gb", "1m"])
     ap.add_argument("--chunk", type=int, default=10000)
-    ap.add_argument("--seg-records", type=int, default=2_621_440)   # ~1 GB of text per segment
-    ap.add_argument("--repeats", type=int, default=203)             # per GPU: ~50 GB gz, ~532 M records
+    # the 50 GB member repeats one segment of distinct text: 10.5 M records (~4 GB of text, ~1 GB of
+    # gzip) x 51 = ~50 GB gz, ~535 M records (r01: a 1 GB segment x 203)
+    ap.add_argument("--seg-records", type=int, default=None, help=f"records per segment (default {SEG_RECORDS:,})")
+    ap.add_argument("--repeats", type=int, default=REPEATS)          # per GPU (weak) or in all (strong)
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default for N > 1, BASELINE configs[3]): one ~50 GB member split over the N "
                          "GPUs; weak: ~50 GB of gzip per GPU")
@@ -458,6 +463,8 @@ def main():
                          "ingest, PCIe-inclusive; reported under 'ingest', never as value)")
     ap.add_argument("--ingest", action="store_true", help=argparse.SUPPRESS)   # on by default since r02
     args = ap.parse_args()
+    if args.seg_records is None:   # the paired files keep 1 GB segments: two members must fit one GPU
+        args.seg_records = PAIRED_SEG_RECORDS if args.paired else SEG_RECORDS
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -600,7 +607,8 @@ def main():
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member, zlib level 6)"
+        "data": f"synthetic (Generator-shape 150 bp FASTQ, tiled single gzip member: one {tf.text_len / 1e9:.1f} GB "
+                f"text segment x {tf.repeats}, zlib level 6)"
                 + (", an empty line after every record (side measurement)" if args.blank_lines else ""),
         "config": {"workload": workload,
                    "records": total_records, "gz_bytes": tf.file_len, "decompressed_bytes": text_bytes,

@@ -83,7 +83,7 @@ def test_configs2_full_50gb_member_on_device(device):
     sys.path.insert(0, ROOT)
     import bench
     from parallelparsing_amd.tiled import TiledFile
-    tf = TiledFile(2_621_440, 203, 10000, threads=16)         # bench.py's default workload
+    tf = TiledFile(bench.SEG_RECORDS, bench.REPEATS, 10000, threads=16)   # bench.py's default workload
     assert tf.file_len > 49e9
     dev = torch.device("cuda", device.device)
     n = tf.npoints - 1
