@@ -455,6 +455,9 @@ def main():
                          "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
                          "0 (default) = auto: enough waves for ~6 generations of the GPU's wave slots (S = 1 for "
                          "the default 50 GB-per-GPU workload, 8 for a strong-scaled rank at N = 8)")
+    ap.add_argument("--share", type=int, default=1,
+                    help="rehearsal on one GPU: decode only rank 0's chunk range of an N-way strong split (the "
+                         "per-rank step of configs[3] at N GPUs, without the other ranks); records checked per range")
     ap.add_argument("--blank-lines", action="store_true",
                     help="side measurement: an empty line after every record, so every chunk takes the declined-chunk "
                          "parse (ppg_parse_chain; PPG_PARSE_CHAIN=0: the byte-serial lane) -- not the metric's workload")
@@ -514,6 +517,10 @@ def main():
     nchunks = tf.npoints - 1
     ranges = partition_chunks(ix_in, world)
     a, b = ranges[rank]
+    if args.share > 1:   # rehearsal: one GPU times rank 0's share of an N-way strong split, alone
+        assert world == 1, "--share emulates one rank of a larger job on a single process"
+        a, b = partition_chunks(ix_in, args.share)[0]
+        ranges = [(a, b)]
     lo, hi = int(ix_in[a]) - 1, int(ix_in[b])   # file bytes [Input_a - 1, Input_b - 1]
     comp_len = hi - lo
     t = time.time()
@@ -581,7 +588,10 @@ def main():
     else:
         total_records = local_records
     expect = tf.expected_records()   # includes the reference's Q1 duplicates
-    if not os.environ.get("PPG_PROBE_NO_CENSUS"):   # an A/B timing probe produces no records
+    if args.share > 1:
+        expect = None   # a share: produced lengths and statuses are checked above, counts per range below
+        line_share = {"share_of": args.share, "chunks": [a, b], "records": total_records}
+    if expect is not None and not os.environ.get("PPG_PROBE_NO_CENSUS"):   # an A/B probe produces no records
         assert total_records == expect, (total_records, expect)
 
     text_bytes = int(ix_out[-1] - ix_out[0])
@@ -629,9 +639,10 @@ def main():
                          "descriptors": 16 * local_records // shard.batches,
                          "parse_reread": 0}},   # the newline census is fused into the inflate flush
         "reference_published_rec_s": REFERENCE_REC_S,
+        **({"rehearsal_share": line_share} if args.share > 1 else {}),
         "communicator": dict(rccl_info(world, backend), count_gather=gather_via),
     }
-    args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines
+    args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines and args.share == 1
     if rank == 0 and world == 1 and (args.ingest or args.create_index):
         del shard, comp
         torch.cuda.empty_cache()
