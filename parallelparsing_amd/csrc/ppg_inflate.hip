@@ -54,6 +54,14 @@
 #ifndef PPG_TAIL_PRIO
 #define PPG_TAIL_PRIO 1
 #endif
+// the other serial stretches of the decoder: a bit-serial token (long code, end-of-block) and a
+// dynamic block header (code lengths, tables): 810.1 -> 805.9 ms with both at 2 (r02, near noise)
+#ifndef PPG_SPEC_PRIO
+#define PPG_SPEC_PRIO 2
+#endif
+#ifndef PPG_HDR_PRIO
+#define PPG_HDR_PRIO 2
+#endif
 #endif
 #ifndef PPG_POST_WALK_PRIO
 #ifdef PPG_EMIT_PRIO
@@ -617,6 +625,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             build_table<DB>(S.lens + 288, 32, S.dst, &cdst, S.dst_sorted, TAB_DST, lane);
         } else {
             // ---- dynamic Huffman codes (RFC 1951 3.2.7) ----
+#ifdef PPG_HDR_PRIO
+            asm volatile("s_setprio " PPG_STR(PPG_HDR_PRIO));
+#endif
             rd_refill(r, S.stream, lane);
             const uint32_t hlit = br_take(r, 5) + 257, hdist = br_take(r, 5) + 1, hclen = br_take(r, 4) + 4;
             if (hlit > 286 || hdist > 30) { status = ST_DATA_ERROR; break; }
@@ -659,6 +670,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, &cdst, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
         }
         in_block = 1;
+#ifdef PPG_HDR_PRIO
+        asm volatile("s_setprio 0");
+#endif
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
         // through the outer loop), so the token rounds keep it in SGPRs with scalar branches
         r.sg = uni(r.sg);
@@ -913,6 +927,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             }
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
+#ifdef PPG_SPEC_PRIO
+            asm volatile("s_setprio " PPG_STR(PPG_SPEC_PRIO));
+#endif
             rd_seek(r, S.stream, bp, lane);
             rd_refill(r, S.stream, lane);
             const int sym = canon_decode(r, clit, S.lit_sorted, lane);
@@ -943,6 +960,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
+#ifdef PPG_SPEC_PRIO
+            asm volatile("s_setprio 0");
+#endif
             if (pos >= len) break;
         }
         if (status != ST_OK) break;
