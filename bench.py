@@ -631,6 +631,11 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload, shard.batches),
                      "kernel": "ppg_inflate_kernel", "alg_bytes_per_launch": alg_local / shard.batches,
                      "mean_launch_ms": mean_launch_s * 1e3,
+                     # memory-side bytes (2 x FETCH_SIZE + WRITE_SIZE, calibrated, Infinity-Cache hits
+                     # included) over the same launch time: how much of the HBM peak the traffic is
+                     **({"traffic_GBps": traffic / mean_launch_s / 1e9,
+                         "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS}
+                        if (traffic := pmc_traffic(workload, shard.batches)) else {}),
                      # SURVEY §8d's secondary terms (not in alg_bytes), per launch of this rank
                      "secondary_bytes_per_launch": {
                          "windows": 32768 * (b - a + n_side) // shard.batches,
