@@ -189,7 +189,7 @@ def create_index_run(tf, args, dev):
     for _ in range(2):                                             # first run: allocation warm-up
         ix = None
         t = time.perf_counter()
-        ix = pp.Core.BuildDeflateIndexGpu(g, args.chunk)
+        ix = pp.Core.BuildDeflateIndexGpu(g, args.chunk, out_capacity=int(args.ix_capacity_gib * (1 << 30)))
         runs.append(time.perf_counter() - t)
         log(f"[bench] GPU CreateIndex: {runs[-1]:.2f} s, {ix.Count} points")
     st = pp.Core.gpu_index_stats()
@@ -224,6 +224,7 @@ def create_index_run(tf, args, dev):
                                                        "census_ms")},
             "pieces": int(st["pieces"]), "real_pieces": int(st["real_pieces"]), "redo1": int(st["redo1"]),
             "pass2_batches": int(st["batches"]),
+            "pass2_capacity": f"{args.ix_capacity_gib:g} GiB" if args.ix_capacity_gib else "default (96 GiB or free HBM - 4 GiB)",
             "blocks": int(st["blocks"]), "verified": "every Point (Output, Input, Bits, Window, offset) of the member",
             "cpu_reference": {"seconds": csec, "decompressed_GBps": cpu_gbs, "cores": 1,
                               "sample": f"host zlib CreateIndex (Core.cs:14-131 restated) of a 1-segment member "
@@ -337,15 +338,16 @@ def wave_slots(dev):
 
 def auto_split(args, slots, chunks):
     """(S, K): split the last K of a rank's chunks into up to S waves each (ppg_shard_set_split).
-    --split S > 0: every chunk.  --split 0 (auto): a rank holding fewer than ~6 generations of
-    resident waves (CUs x 32) splits every chunk, into enough waves for ~6 generations (at most 64:
-    in practice every inner block start, ~15 per 10k-record chunk);
-    a larger rank splits only its last generation, into 4, so the launch's tail drains in a
-    quarter of a chunk's time.  Measured on one MI355X."""
+    --split S > 0: every chunk.  --split 0 (auto): a rank holding less than one generation of
+    resident waves (CUs x 32; --split-gens) splits every chunk, into enough waves for ~6
+    generations and at least --tail-split (at most 64: in practice every inner block start, ~15 per
+    10k-record chunk); a larger rank splits only its last half-generation (--tail-gens) into
+    --tail-split = 8, so the launch's tail drains in an eighth of a chunk's time.  Measured on one
+    MI355X for the N = 1 step and the N = 2/4/8 strong-scaling shares."""
     if args.split > 0:
         return args.split, chunks
-    if chunks < 6 * slots:
-        return int(min(64, max(1, -(-6 * slots // max(1, chunks))))), chunks
+    if chunks < getattr(args, "split_gens", 1) * slots:
+        return int(min(64, max(args.tail_split, -(-6 * slots // max(1, chunks))))), chunks
     return args.tail_split, min(chunks, int(args.tail_gens * slots))
 
 
@@ -441,11 +443,16 @@ def main():
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ix-capacity-gib", type=float, default=0,
+                    help="--create-index: pass-2 output buffer in GiB (0 = the library's default)")
     ap.add_argument("--create-index", action="store_true",
                     help="also time the GPU CreateIndex over the whole member (reported under 'create_index')")
     ap.add_argument("--paired", action="store_true",
                     help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
     ap.add_argument("--paired-repeats", type=int, default=0)   # 0: 51 (~12.5 GB gz per file) on 1 GPU, 102 for N > 1
+    ap.add_argument("--split-gens", type=float, default=1,
+                    help="--split 0: a rank with fewer chunks than this many generations of wave slots splits every "
+                         "chunk; a larger one splits its last --tail-gens generations into --tail-split waves")
     ap.add_argument("--tail-split", type=int, default=8,
                     help="--split 0 on a large rank: waves per chunk for its last generation of chunks (1 = off)")
     ap.add_argument("--tail-gens", type=float, default=0.5,
@@ -453,8 +460,8 @@ def main():
     ap.add_argument("--split", type=int, default=0,
                     help="decode each chunk as up to S waves, split at inner deflate block starts "
                          "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
-                         "0 (default) = auto: enough waves for ~6 generations of the GPU's wave slots (S = 1 for "
-                         "the default 50 GB-per-GPU workload, 8 for a strong-scaled rank at N = 8)")
+                         "0 (default) = auto (auto_split): the last half-generation of a rank's chunks into 8 waves "
+                         "each; every chunk, into >= 8, on a rank with less than one generation (N = 8 strong)")
     ap.add_argument("--share", type=int, default=1,
                     help="rehearsal on one GPU: decode only rank 0's chunk range of an N-way strong split (the "
                          "per-rank step of configs[3] at N GPUs, without the other ranks); records checked per range")

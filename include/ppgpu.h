@@ -58,7 +58,8 @@ int ppg_index_build_mem(const uint8_t *gz, int64_t gz_len, uint32_t chunksize, p
  * Decompressor/Core.cs:14-131) from a block-parallel decode (ppg_index_gpu.cpp): candidate block
  * headers per piece of piece_bytes (0: automatic), a verified chain of block ends, exact output
  * per piece, then the '@' census.  gz: the whole single-member .gz, in host memory or (gz_on_device,
- * 4-byte aligned) in device memory.  out_capacity bounds the exact-output buffer (0: free HBM).
+ * 4-byte aligned) in device memory.  out_capacity bounds the exact-output buffer (0: 96 GiB or free HBM less 4 GiB,
+ * whichever is smaller; larger members are decoded in batches).
  * Returns PPG_UNSUPPORTED for zlib-wrapped / multi-member input (use ppg_index_build_file). */
 int ppg_index_build_gpu(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
                         int64_t piece_bytes, int64_t out_capacity, ppg_index **out);

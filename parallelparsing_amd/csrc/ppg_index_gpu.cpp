@@ -61,9 +61,17 @@ namespace {
 
 constexpr uint64_t kRing = 65536;       // pass-1 output ring per piece (IX_RING_BYTES)
 constexpr int64_t kMaxRun = kWin;       // at most 32768 bytes since the last '@'
+constexpr uint64_t kPass2Cap = 96ull << 30;   // default pass-2 output buffer
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// capacity for `need` elements, reserved as need x max(scale, 1.5) when it has to grow
+template <class V>
+void grow(V &v, size_t need, double scale) {
+    if (need <= v.capacity()) return;
+    v.reserve(std::max<size_t>(need, (size_t)((double)need * std::max(scale, 1.5))));
+}
 
 // RFC 1952 member header length, or -1 (not a gzip member this path handles)
 int64_t gzip_header_len(const uint8_t *h, int64_t n) {
@@ -404,7 +412,10 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         size_t fr = 0, tot = 0;
         HIPCHK(hipMemGetInfo(&fr, &tot));
         const uint64_t avail = fr > (4ull << 30) ? (uint64_t)fr - (4ull << 30) : (uint64_t)fr / 2;
-        cap = std::min<uint64_t>(total, avail);
+        // 96 GiB by default: a 204 GB buffer (the whole 50 GB member) cost 2.07 s of hipMalloc when
+        // the previous call's had just been freed; two 96 GiB batches decode in 5.47 s both times
+        // (bench.py --create-index --ix-capacity-gib, r02)
+        cap = std::min<uint64_t>(std::min<uint64_t>(total, avail), kPass2Cap);
     }
     cap = std::max<uint64_t>(cap, max_u);
     DevBuf<uint8_t> out;
@@ -569,11 +580,14 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         const size_t hw_n = gw.size() * kWin;
         std::unique_ptr<uint8_t[]> hw_buf(new uint8_t[std::max<size_t>(hw_n, 1)]);
         uint8_t *const hw = hw_buf.get();
-        ix.pts.reserve(ix.pts.size() + picks.size());
-        ix.windows.reserve(ix.windows.size() + picks.size() * kWin);
-        ix.side_bit.reserve(ix.side_bit.size() + sides.size());
-        ix.side_out.reserve(ix.side_out.size() + sides.size());
-        ix.side_win.reserve(ix.side_win.size() + sides.size() * kWin);
+        // grown to the whole member's projected size (at least x1.5): an exact per-batch reserve
+        // recopied every window so far on every batch (quadratic in the batch count)
+        const double proj = 1.02 * (double)total / (double)std::max<uint64_t>(O[b1], 1);
+        grow(ix.pts, ix.pts.size() + picks.size(), proj);
+        grow(ix.windows, ix.windows.size() + picks.size() * kWin, proj);
+        grow(ix.side_bit, ix.side_bit.size() + sides.size(), proj);
+        grow(ix.side_out, ix.side_out.size() + sides.size(), proj);
+        grow(ix.side_win, ix.side_win.size() + sides.size() * kWin, proj);
         if (!gw.empty()) {
             HIPCHK(B.gat.alloc(gw.size()));
             HIPCHK(dwin.alloc(gw.size() * kWin));
