@@ -35,3 +35,15 @@ def test_tail_knobs():
     assert bench.auto_split(args(tail_split=1), SLOTS, 60000) == (1, 4096)   # off: S = 1
     assert bench.auto_split(args(tail_gens=2.0), SLOTS, 60000) == (8, 16384)
     assert bench.auto_split(args(split_gens=6), SLOTS, 26498) == (8, 26498)   # the r01 rule, floor 8
+
+
+def test_tail2_split():
+    a = args()
+    a.tail2 = "16:0.25"
+    a.split = 8
+    assert bench.tail2_split(a, SLOTS, 4096) == (16, 2048)     # N = 1: the last quarter generation into 16
+    assert bench.tail2_split(a, SLOTS, 1000) == (16, 1000)     # fewer split chunks than that: all of them
+    a.tail2 = "off"
+    assert bench.tail2_split(a, SLOTS, 4096) == (8, 0)
+    a.tail2, a.split = "4:0.25", 8                              # not finer than the split: no second stage
+    assert bench.tail2_split(a, SLOTS, 4096) == (8, 0)
