@@ -223,6 +223,7 @@ def create_index_run(tf, args, dev):
             "phases_ms": {k: round(st[k], 2) for k in ("finder_ms", "pass1_ms", "chain_ms", "resolve_ms", "pass2_ms", "pass2_alloc_ms",
                                                        "census_ms")},
             "pieces": int(st["pieces"]), "real_pieces": int(st["real_pieces"]), "redo1": int(st["redo1"]),
+            "spec_redos": int(st["spec_redos"]), "serial_redos": int(st["serial_redos"]),
             "pass2_batches": int(st["batches"]),
             "pass2_capacity": f"{args.ix_capacity_gib:g} GiB" if args.ix_capacity_gib else "default (96 GiB or free HBM - 4 GiB)",
             "blocks": int(st["blocks"]), "verified": "every Point (Output, Input, Bits, Window, offset) of the member",

@@ -79,7 +79,9 @@ int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksi
 /* Last GPU CreateIndex on ctx: [0] finder ms, [1] pass-1 ms, [2] chain check ms, [3] pass-2 ms,
  * [4] census + windows ms, [5] total ms, [6] pieces, [7] real pieces, [8] pass-1 redos,
  * [9] history resolve ms, [10] pass-2 batches, [11] blocks, [12] points, [13] output bytes,
- * [14] file upload ms (ppg_index_build_gpu_file). */
+ * [14] file upload ms (ppg_index_build_gpu_file), [15] pass-2 buffer allocation ms,
+ * [16] speculative redos (false starts decoded again from their predecessor's end, one launch),
+ * [17] serial redos (false starts the speculation missed).  n <= 18 values are written. */
 int ppg_index_build_gpu_stats(ppg_ctx *ctx, double *vals, int32_t n);
 
 /* Serialize / Deserialize — Common/IndexIO.cs:7-27 / :29-53 (byte-identical .gzi format). */

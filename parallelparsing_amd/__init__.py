@@ -321,14 +321,14 @@ class Core:
 
     GPU_INDEX_STATS = ("finder_ms", "pass1_ms", "chain_ms", "pass2_ms", "census_ms", "total_ms", "pieces",
                        "real_pieces", "redo1", "resolve_ms", "batches", "blocks", "points", "output_bytes",
-                       "upload_ms", "pass2_alloc_ms")
+                       "upload_ms", "pass2_alloc_ms", "spec_redos", "serial_redos")
 
     @staticmethod
     def gpu_index_stats(device=None):
         """Timings and counts of the last BuildDeflateIndexGpu on a device (ppg_index_build_gpu_stats)."""
         dev = device or Device.default()
-        v = (C.c_double * 16)()
-        check(lib.ppg_index_build_gpu_stats(dev.handle, v, 16), "ppg_index_build_gpu_stats")
+        v = (C.c_double * len(Core.GPU_INDEX_STATS))()
+        check(lib.ppg_index_build_gpu_stats(dev.handle, v, len(v)), "ppg_index_build_gpu_stats")
         return dict(zip(Core.GPU_INDEX_STATS, list(v)))
 
     @staticmethod

@@ -70,6 +70,8 @@ struct ppg_index {
 
 struct IngestState;   // host-ingest buffers kept across ppg_file_decompress_all calls
 
+constexpr int kIxStats = 18;   // ppg_index_build_gpu_stats values (parallelparsing_amd.Core.GPU_INDEX_STATS)
+
 struct ppg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -77,7 +79,7 @@ struct ppg_ctx {
     IngestState *ingest = nullptr;
     int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
     int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)
-    double ix_stats[16] = {0};   // timings / counts of the last GPU CreateIndex (ppg_index_build_gpu_stats)
+    double ix_stats[kIxStats] = {0};   // timings / counts of the last GPU CreateIndex (ppg_index_build_gpu_stats)
 };
 
 template <class T>

@@ -62,6 +62,7 @@ namespace {
 constexpr uint64_t kRing = 65536;       // pass-1 output ring per piece (IX_RING_BYTES)
 constexpr int64_t kMaxRun = kWin;       // at most 32768 bytes since the last '@'
 constexpr uint64_t kPass2Cap = 96ull << 30;   // default pass-2 output buffer
+constexpr uint32_t kSpare = 256;        // pass-1 slots for speculative redos of false starts
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
@@ -135,10 +136,8 @@ struct Builder {
     std::vector<PpgInflateJob> hjobs;
     std::vector<PpgInflateResult> hres;
     std::vector<PpgBlockEnd> hblk;
-    DevBuf<PpgInflateJob> jobs;
-    DevBuf<PpgInflateResult> res;
-    DevBuf<PpgBlockEnd> blk, bigblk;
-    DevBuf<uint8_t> ring;
+    DevBuf<PpgBlockEnd> blk, bigblk;   // block lists: history A at blk_off, B at blk_off + blk_half
+    DevBuf<uint8_t> ring;               // 64 KiB output ring per slot and history
     DevBuf<uint8_t> pat;                // synthetic histories A (offset 0) and B (offset 32 KiB)
     DevBuf<uint8_t> ta, tb;             // tails of pass-1 job q at q * 32 KiB, runs A and B
     std::vector<PpgInflateResult> hres_b;
@@ -147,44 +146,55 @@ struct Builder {
     DevBuf<uint64_t> dpre;
     DevBuf<PpgBlockEnd> dense;
 
-    // pass-1 decode of job slots `which` (ascending), once per synthetic history; refreshes
-    // their results, block lists and both tails
+    uint32_t nslots = 0;                // pieces + spare slots for speculative redos
+    uint64_t blk_half = 0;              // history B's block lists sit at blk_off + blk_half (never read)
+    DevBuf<PpgInflateJob> jst;          // staged jobs of a pass-1 launch: [A..., B...]
+    DevBuf<PpgInflateResult> rst;
+
+    // pass-1 decode of job slots `which` (ascending), both synthetic histories in one launch
+    // (history A: ring slot q, history B: ring slot nslots + q); refreshes their results, block
+    // lists and both tails
     int run_pass1(const std::vector<uint32_t> &which, bool big) {
         if (which.empty()) return PPG_OK;
-        for (int run = 0; run < 2; run++) {
-            std::vector<PpgInflateResult> &hr = run ? hres_b : hres;
-            for (uint32_t q : which) hjobs[q].dict_off = run ? (uint64_t)kWin : 0;
-            // contiguous runs launch as one grid; the common case is all slots at once
-            for (size_t i = 0; i < which.size();) {
-                size_t e = i + 1;
-                while (e < which.size() && which[e] == which[e - 1] + 1 && !big) e++;
-                const uint32_t q0 = which[i], n = (uint32_t)(e - i);
-                HIPCHK(hipMemcpyAsync(jobs.p + q0, hjobs.data() + q0, sizeof(PpgInflateJob) * n, hipMemcpyHostToDevice,
-                                      s));
-                HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jobs.p + q0, pat.p, ring.p, res.p + q0,
-                                             big ? bigblk.p : blk.p, (int)n));
-                HIPCHK(hipMemcpyAsync(hr.data() + q0, res.p + q0, sizeof(PpgInflateResult) * n, hipMemcpyDeviceToHost,
-                                      s));
-                i = e;
-            }
-            HIPCHK(hipStreamSynchronize(s));
-            // this run's tails (before the next run reuses the rings)
-            std::vector<PpgGather> g(which.size());
-            for (size_t i = 0; i < which.size(); i++) {
-                const uint32_t q = which[i];
-                g[i] = PpgGather{(uint64_t)q * kRing, run ? (uint64_t)kWin : 0, hr[q].produced, kRing - 1, 0};
-            }
-            HIPCHK(gat.alloc(g.size()));
-            HIPCHK(hipMemcpyAsync(gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
-            uint8_t *tails = run ? tb.p : ta.p;
-            for (size_t i = 0; i < which.size();) {   // one gather per contiguous run of slots
-                size_t e = i + 1;
-                while (e < which.size() && which[e] == which[e - 1] + 1) e++;
-                HIPCHK(ppg_launch_gather(s, ring.p, pat.p, gat.p + i, tails + (uint64_t)which[i] * kWin, nullptr,
-                                         nullptr, (int)(e - i)));
-                i = e;
-            }
-            HIPCHK(hipStreamSynchronize(s));
+        const size_t n = which.size();
+        std::vector<PpgInflateJob> st(2 * n);
+        for (size_t i = 0; i < n; i++) {
+            PpgInflateJob a = hjobs[which[i]];
+            a.dict_off = 0;
+            st[i] = a;
+            a.dict_off = kWin;
+            a.out_off = (uint64_t)(nslots + which[i]) * kRing;
+            a.blk_off = big ? a.blk_cap : (uint32_t)(a.blk_off + blk_half);
+            st[n + i] = a;
+        }
+        HIPCHK(jst.alloc(2 * n));
+        HIPCHK(rst.alloc(2 * n));
+        HIPCHK(hipMemcpyAsync(jst.p, st.data(), sizeof(PpgInflateJob) * 2 * n, hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jst.p, pat.p, ring.p, rst.p, big ? bigblk.p : blk.p, (int)(2 * n)));
+        std::vector<PpgInflateResult> r(2 * n);
+        HIPCHK(hipMemcpyAsync(r.data(), rst.p, sizeof(PpgInflateResult) * 2 * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (size_t i = 0; i < n; i++) {
+            hres[which[i]] = r[i];
+            hres_b[which[i]] = r[n + i];
+        }
+        // both runs' tails (run A's ring slots, then run B's)
+        std::vector<PpgGather> g(2 * n);
+        for (size_t i = 0; i < n; i++) {
+            const uint32_t q = which[i];
+            g[i] = PpgGather{(uint64_t)q * kRing, 0, hres[q].produced, kRing - 1, 0};
+            g[n + i] = PpgGather{(uint64_t)(nslots + q) * kRing, (uint64_t)kWin, hres_b[q].produced, kRing - 1, 0};
+        }
+        HIPCHK(gat.alloc(g.size()));
+        HIPCHK(hipMemcpyAsync(gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
+        for (size_t i = 0; i < n;) {   // one gather per contiguous run of slots and history
+            size_t e = i + 1;
+            while (e < n && which[e] == which[e - 1] + 1) e++;
+            HIPCHK(ppg_launch_gather(s, ring.p, pat.p, gat.p + i, ta.p + (uint64_t)which[i] * kWin, nullptr, nullptr,
+                                     (int)(e - i)));
+            HIPCHK(ppg_launch_gather(s, ring.p, pat.p, gat.p + n + i, tb.p + (uint64_t)which[i] * kWin, nullptr,
+                                     nullptr, (int)(e - i)));
+            i = e;
         }
         for (uint32_t q : which) {   // both runs follow the same bits: same blocks, same sizes
             const PpgInflateResult &a = hres[q], &b = hres_b[q];
@@ -197,25 +207,18 @@ struct Builder {
             hblk_big.assign(nb, PpgBlockEnd{0, 0});
             if (nb) HIPCHK(hipMemcpyAsync(hblk_big.data(), bigblk.p, sizeof(PpgBlockEnd) * nb, hipMemcpyDeviceToHost, s));
         } else {
-            // pack the runs' block lists densely on the device, one copy back
-            std::vector<uint64_t> pre(which.size() + 1, 0);
-            for (size_t i = 0; i < which.size(); i++)
-                pre[i + 1] = pre[i] + std::min(hres[which[i]].nblocks, hjobs[which[i]].blk_cap);
+            // pack run A's block lists densely on the device, one copy back
+            std::vector<uint64_t> pre(n + 1, 0);
+            for (size_t i = 0; i < n; i++) pre[i + 1] = pre[i] + std::min(hres[which[i]].nblocks, hjobs[which[i]].blk_cap);
             HIPCHK(dpre.alloc(pre.size()));
             HIPCHK(dense.alloc(pre.back() + 1));
             HIPCHK(hipMemcpyAsync(dpre.p, pre.data(), 8 * pre.size(), hipMemcpyHostToDevice, s));
-            for (size_t i = 0; i < which.size();) {
-                size_t e = i + 1;
-                while (e < which.size() && which[e] == which[e - 1] + 1) e++;
-                HIPCHK(ppg_launch_pack_blocks(s, blk.p, jobs.p + which[i], res.p + which[i], dpre.p + i, dense.p,
-                                              (int)(e - i)));
-                i = e;
-            }
+            HIPCHK(ppg_launch_pack_blocks(s, blk.p, jst.p, rst.p, dpre.p, dense.p, (int)n));
             std::vector<PpgBlockEnd> hd(pre.back());
             if (!hd.empty())
                 HIPCHK(hipMemcpyAsync(hd.data(), dense.p, sizeof(PpgBlockEnd) * hd.size(), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
-            for (size_t i = 0; i < which.size(); i++)
+            for (size_t i = 0; i < n; i++)
                 std::copy(hd.begin() + (ptrdiff_t)pre[i], hd.begin() + (ptrdiff_t)pre[i + 1],
                           hblk.begin() + hjobs[which[i]].blk_off);
         }
@@ -239,7 +242,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
                            int64_t side_bytes, ppg_index &ix) {
     const auto t_all = Clock::now();
     double *stat = ctx->ix_stats;
-    std::fill(stat, stat + 16, 0.0);
+    std::fill(stat, stat + kIxStats, 0.0);
     const int64_t hl = gzip_header_len(head, head_n);
     if (hl < 0 || len < hl + 8 + 1) return PPG_UNSUPPORTED;
     Builder B;
@@ -285,11 +288,15 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
 
     // ---- 2. pass 1: block ends + speculative tails ----
     t = Clock::now();
-    B.hjobs.resize(m);
-    B.hres.assign(m, PpgInflateResult{});
-    B.hres_b.assign(m, PpgInflateResult{});
-    B.own_blocks.assign(m, {});
+    // slots [0, m): the pieces; [m, m + kSpare): speculative redos (below)
+    const uint32_t nslots = m + kSpare;
+    B.nslots = nslots;
+    B.hjobs.resize(nslots);
+    B.hres.assign(nslots, PpgInflateResult{});
+    B.hres_b.assign(nslots, PpgInflateResult{});
+    B.own_blocks.assign(nslots, {});
     uint64_t nblk_total = 0;
+    uint32_t max_cap = 0;
     for (uint32_t q = 0; q < m; q++) {
         const uint64_t stop = q + 1 < m ? pieces[q + 1].start : ~0ull;
         const uint64_t span = (q + 1 < m ? stop : end_bits) - pieces[q].start;
@@ -304,16 +311,19 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         J.blk_off = (uint32_t)nblk_total;
         if (span >= (1ull << 31)) return PPG_UNSUPPORTED;   // the decoder's piece-relative bit positions are 32-bit
         J.blk_cap = (uint32_t)std::min<uint64_t>(span / 8 / 2048 + 64, 1u << 24);
+        max_cap = std::max(max_cap, J.blk_cap);
         nblk_total += J.blk_cap;
-        if (nblk_total >= (1ull << 31)) return PPG_UNSUPPORTED;
     }
+    const uint32_t spare_cap = std::min<uint32_t>(2 * max_cap, 1u << 24);
+    const uint64_t spare_blk = nblk_total;
+    nblk_total += (uint64_t)kSpare * spare_cap;
+    if (nblk_total >= (1ull << 31)) return PPG_UNSUPPORTED;
+    B.blk_half = nblk_total;
     B.hblk.assign(nblk_total, PpgBlockEnd{0, 0});
-    HIPCHK(B.jobs.alloc(m));
-    HIPCHK(B.res.alloc(m));
-    HIPCHK(B.blk.alloc(nblk_total));
-    HIPCHK(B.ring.alloc((size_t)m * kRing));
-    HIPCHK(B.ta.alloc((size_t)m * kWin));
-    HIPCHK(B.tb.alloc((size_t)m * kWin));
+    HIPCHK(B.blk.alloc(2 * nblk_total));
+    HIPCHK(B.ring.alloc((size_t)2 * nslots * kRing));
+    HIPCHK(B.ta.alloc((size_t)nslots * kWin));
+    HIPCHK(B.tb.alloc((size_t)nslots * kWin));
     {
         std::vector<uint8_t> pat(2 * kWin);
         for (int i = 0; i < kWin; i++) {
@@ -334,6 +344,44 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     // walk the pieces in order: a piece is real iff its predecessor (real) ended at its start
     t = Clock::now();
     int redo1 = 0;
+    // the first piece after piece j's last block end E: pieces starting inside that block are false
+    // starts and are dropped
+    auto next_piece = [&](size_t j, uint64_t E) {
+        size_t k = j + 1;
+        while (k < pieces.size() && pieces[k].start < E && (k + 1 >= pieces.size() || pieces[k + 1].start <= E)) k++;
+        return k;
+    };
+    // Speculative redos, one launch: every piece k whose predecessor j (if real) ends somewhere
+    // else than k starts is decoded again from that end, into a spare slot.  The walk below takes a
+    // spare when it reaches k from the same end; a wrong guess (j itself a false start) is never
+    // reached, and a false start beyond the spares is redone serially there.
+    std::vector<std::pair<uint64_t, uint32_t>> spec(m, {~0ull, 0});   // piece k -> (E, spare slot)
+    {
+        std::vector<uint32_t> spares;
+        for (size_t j = 0; j + 1 < m && spares.size() < kSpare; j++) {
+            const PpgInflateResult &r = B.hres[j];
+            if (r.status != PPG_OK || r.nblocks == 0 || r.last || (r.flags & PPG_FLAG_BLK_FULL)) continue;
+            uint32_t nb = 0;
+            const uint64_t E = B.blocks((uint32_t)j, nb)[nb - 1].end_bit;
+            const size_t k = next_piece(j, E);
+            if (k >= m || pieces[k].start == E || spec[k].first != ~0ull) continue;
+            const uint32_t q = m + (uint32_t)spares.size();
+            PpgInflateJob J = B.hjobs[pieces[k].slot];
+            J.bit_start = E;
+            if (J.stop_bit != ~0ull && J.stop_bit <= E) J.stop_bit = E + 1;
+            const uint64_t span = (J.stop_bit != ~0ull ? J.stop_bit : end_bits) - E;
+            if (span >= (1ull << 31)) continue;
+            J.out_off = (uint64_t)q * kRing;
+            J.blk_off = (uint32_t)(spare_blk + (uint64_t)(q - m) * spare_cap);
+            J.blk_cap = spare_cap;
+            B.hjobs[q] = J;
+            spec[k] = {E, q};
+            spares.push_back(q);
+        }
+        int rc = B.run_pass1(spares, false);
+        if (rc) return rc;
+        stat[16] = (double)spares.size();
+    }
     std::vector<Piece> real;
     {
         size_t j = 0;
@@ -346,7 +394,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
                 const uint64_t span = (J.stop_bit != ~0ull ? J.stop_bit : end_bits) - J.bit_start;
                 J.blk_off = 0;
                 J.blk_cap = (uint32_t)std::min<uint64_t>(span / 10 + 64, 1u << 30);
-                HIPCHK(B.bigblk.alloc(J.blk_cap));
+                HIPCHK(B.bigblk.alloc(2 * (size_t)J.blk_cap));   // histories A and B
                 int rc = B.run_pass1({q}, true);
                 if (rc) return rc;
                 B.own_blocks[q] = B.hblk_big;
@@ -359,20 +407,23 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             uint32_t nb = 0;
             const PpgBlockEnd *bl = B.blocks(q, nb);
             const uint64_t E = bl[nb - 1].end_bit;
-            // pieces starting inside piece j's last block are false starts: drop them
-            size_t k = j + 1;
-            while (k < pieces.size() && pieces[k].start < E && (k + 1 >= pieces.size() || pieces[k + 1].start <= E)) k++;
+            const size_t k = next_piece(j, E);
             if (k >= pieces.size()) return PPG_DATA_ERROR;   // a non-final piece must be followed by one
             if (pieces[k].start != E) {
-                // false start: decode piece k again from the real block end
-                pieces[k].start = E;
-                PpgInflateJob &J = B.hjobs[pieces[k].slot];
-                J.bit_start = E;
-                B.own_blocks[pieces[k].slot].clear();
-                if (J.stop_bit != ~0ull && J.stop_bit <= E) J.stop_bit = E + 1;
-                int rc = B.run_pass1({pieces[k].slot}, false);
-                if (rc) return rc;
                 redo1++;
+                if (spec[k].first == E) {
+                    pieces[k] = Piece{spec[k].second, E};       // decoded from E already
+                } else {
+                    // false start: decode piece k again from the real block end
+                    pieces[k].start = E;
+                    PpgInflateJob &J = B.hjobs[pieces[k].slot];
+                    J.bit_start = E;
+                    B.own_blocks[pieces[k].slot].clear();
+                    if (J.stop_bit != ~0ull && J.stop_bit <= E) J.stop_bit = E + 1;
+                    int rc = B.run_pass1({pieces[k].slot}, false);
+                    if (rc) return rc;
+                    stat[17] += 1;                              // serial redos (no spare)
+                }
             }
             j = k;
         }
@@ -758,7 +809,7 @@ int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksi
 
 int ppg_index_build_gpu_stats(ppg_ctx *ctx, double *vals, int32_t n) {
     if (!ctx || !vals || n < 0) return PPG_ARG_ERROR;
-    for (int32_t i = 0; i < n && i < 16; i++) vals[i] = ctx->ix_stats[i];
+    for (int32_t i = 0; i < n && i < kIxStats; i++) vals[i] = ctx->ix_stats[i];
     return PPG_OK;
 }
 
