@@ -35,6 +35,7 @@
 #include "ppg_host.h"
 #include <zlib.h>
 #include <chrono>
+#include <cstdlib>
 #include <memory>
 #include <fcntl.h>
 #include <unistd.h>
@@ -63,6 +64,12 @@ constexpr uint64_t kRing = 65536;       // pass-1 output ring per piece (IX_RING
 constexpr int64_t kMaxRun = kWin;       // at most 32768 bytes since the last '@'
 constexpr uint64_t kPass2Cap = 96ull << 30;   // default pass-2 output buffer
 constexpr uint32_t kSpare = 256;        // pass-1 slots for speculative redos of false starts
+
+// spare slots: kSpare, or PPG_IX_SPARES (tests: 0 sends every false start down the serial redo)
+uint32_t spare_slots() {
+    const char *e = getenv("PPG_IX_SPARES");
+    return e && *e ? (uint32_t)std::min(atol(e) < 0 ? 0L : atol(e), 1L << 16) : kSpare;
+}
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
@@ -280,6 +287,13 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         }
         HIPCHK(hipStreamSynchronize(s));
     }
+    if (const char *e = getenv("PPG_IX_PERTURB")) {
+        // test hook: every n-th candidate moved one bit off its block start -- a false start the
+        // chain walk must redo from the real block end (tests/test_index_gpu.py)
+        const long n = atol(e);
+        for (size_t i = 0; n > 0 && i < cand.size(); i++)
+            if (i % (size_t)n == (size_t)n - 1 && cand[i] != ~0ull && cand[i] + 1 < end_bits) cand[i] += 1;
+    }
     std::vector<Piece> pieces{{0, d0}};
     for (uint64_t c : cand)
         if (c != ~0ull) pieces.push_back({(uint32_t)pieces.size(), c});
@@ -288,8 +302,9 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
 
     // ---- 2. pass 1: block ends + speculative tails ----
     t = Clock::now();
-    // slots [0, m): the pieces; [m, m + kSpare): speculative redos (below)
-    const uint32_t nslots = m + kSpare;
+    // slots [0, m): the pieces; [m, m + nspare): speculative redos (below)
+    const uint32_t nspare = spare_slots();
+    const uint32_t nslots = m + nspare;
     B.nslots = nslots;
     B.hjobs.resize(nslots);
     B.hres.assign(nslots, PpgInflateResult{});
@@ -316,7 +331,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     }
     const uint32_t spare_cap = std::min<uint32_t>(2 * max_cap, 1u << 24);
     const uint64_t spare_blk = nblk_total;
-    nblk_total += (uint64_t)kSpare * spare_cap;
+    nblk_total += (uint64_t)nspare * spare_cap;
     if (nblk_total >= (1ull << 31)) return PPG_UNSUPPORTED;
     B.blk_half = nblk_total;
     B.hblk.assign(nblk_total, PpgBlockEnd{0, 0});
@@ -358,7 +373,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     std::vector<std::pair<uint64_t, uint32_t>> spec(m, {~0ull, 0});   // piece k -> (E, spare slot)
     {
         std::vector<uint32_t> spares;
-        for (size_t j = 0; j + 1 < m && spares.size() < kSpare; j++) {
+        for (size_t j = 0; j + 1 < m && spares.size() < nspare; j++) {
             const PpgInflateResult &r = B.hres[j];
             if (r.status != PPG_OK || r.nblocks == 0 || r.last || (r.flags & PPG_FLAG_BLK_FULL)) continue;
             uint32_t nb = 0;

@@ -272,3 +272,24 @@ def test_file_ingest_uses_side_points(piece, tmp_path, device):
     r1, t1, _ = pp.decompress_file(side, str(p), piece_bytes=piece, threads=4, device=device)
     assert t0 == t1 == nrec
     assert (r0 == r1).all()
+
+
+@pytest.mark.parametrize("spares", ["0", "1", ""])
+def test_false_start_redos_speculative_and_serial(spares, device, monkeypatch):
+    """false starts (finder candidates moved off their block starts by PPG_IX_PERTURB) are redone
+    from their predecessor's end either speculatively, all in one launch into spare slots, or serially in the
+    chain walk when the spares run out (PPG_IX_SPARES = 0 / 1 / default 256): the same Points"""
+    monkeypatch.setenv("PPG_IX_SPARES", spares)
+    monkeypatch.setenv("PPG_IX_PERTURB", "3")     # every third finder candidate one bit off
+    total_spec = total_serial = total = 0
+    for name in CASES:
+        meta, gz = load_case(name)
+        _, st = check_both(gz, meta["chunksize"], device, piece_bytes=1024)
+        total += st["redo1"]
+        total_spec += st["spec_redos"]
+        total_serial += st["serial_redos"]
+    assert total > 0
+    if spares == "0":
+        assert total_spec == 0 and total_serial > 0
+    elif spares == "":
+        assert total_spec > 0
