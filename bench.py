@@ -189,7 +189,8 @@ def create_index_run(tf, args, dev):
     for _ in range(2):                                             # first run: allocation warm-up
         ix = None
         t = time.perf_counter()
-        ix = pp.Core.BuildDeflateIndexGpu(g, args.chunk, out_capacity=int(args.ix_capacity_gib * (1 << 30)))
+        ix = pp.Core.BuildDeflateIndexGpu(g, args.chunk, out_capacity=int(args.ix_capacity_gib * (1 << 30)),
+                                          piece_bytes=int(args.ix_piece_kib * 1024))
         runs.append(time.perf_counter() - t)
         log(f"[bench] GPU CreateIndex: {runs[-1]:.2f} s, {ix.Count} points")
     st = pp.Core.gpu_index_stats()
@@ -466,6 +467,8 @@ def main():
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ix-piece-kib", type=float, default=0,
+                    help="--create-index: compressed bytes per pass-1 piece in KiB (0 = the library's default)")
     ap.add_argument("--ix-capacity-gib", type=float, default=0,
                     help="--create-index: pass-2 output buffer in GiB (0 = the library's default)")
     ap.add_argument("--create-index", action="store_true",

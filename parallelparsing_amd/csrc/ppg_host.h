@@ -87,6 +87,11 @@ struct DevBuf {
     T *p = nullptr;
     size_t n = 0;
     ~DevBuf() { if (p) (void)hipFree(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
     hipError_t alloc(size_t count) {
         if (p && n >= count) return hipSuccess;
         if (p) { (void)hipFree(p); p = nullptr; }

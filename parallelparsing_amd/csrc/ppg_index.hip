@@ -254,26 +254,92 @@ hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const P
 // B[i] = ((i >> 8) + 1 + (i & 0xFF)) & 0xFF.  Decoding only copies bytes, so an output byte is
 // either a literal (x == y in both runs) or history byte i (x = A[i], y = B[i], x != y, and
 // i = ((((y - x) & 0xFF) - 1) << 8) | x).  Piece j+1 starts with piece j's last 32 KiB, so
-//   W[j+1][t] = x == y ? x : W[j][i(x, y)],   W[0] = zeros (the stream start),
-// one 32 KiB gather per piece, in piece order (a single workgroup walks the chain).
-__global__ __launch_bounds__(1024) void ppg_resolve_kernel(const uint8_t *__restrict__ ta,
-                                                           const uint8_t *__restrict__ tb,
-                                                           const uint32_t *__restrict__ slots, int np,
-                                                           uint8_t *W) {
-    for (int j = 0; j < np; j++) {
-        const uint8_t *src = W + (uint64_t)j * 32768;
-        uint8_t *dst = W + (uint64_t)(j + 1) * 32768;
+//   W[j+1] = T_j(W[j]),  T_j(W)[t] = x == y ? x : W[i(x, y)],   W[0] = zeros (the stream start).
+// The chain is serial, but the maps compose: as u16 entries (0x8000 | literal, or a history index)
+// T_{j+1} o T_j is again such a map.  So the pieces are cut into G groups of L (G, L ~ sqrt(np)):
+//   compose  (G workgroups)  M_g = T_{last} o ... o T_{first} of group g, in LDS;
+//   groups   (1 workgroup)   W[first of g+1] = M_g(W[first of g]), g = 0..G-1;
+//   fill     (G workgroups)  the W of every piece inside its group, from the group's first.
+// ~3 sqrt(np) dependent 32 KiB steps instead of np (r01-v12 form: one workgroup, np steps).
+__device__ __forceinline__ uint32_t sym_entry(uint32_t x, uint32_t y) {
+    return x == y ? 0x8000u | x : (((((y - x) & 255u) - 1u) << 8) | x) & 0x7FFFu;   // (mask: corrupt data stays in range)
+}
+
+__global__ __launch_bounds__(1024) void ppg_resolve_compose_kernel(const uint8_t *__restrict__ ta,
+                                                                   const uint8_t *__restrict__ tb,
+                                                                   const uint32_t *__restrict__ slots, int np,
+                                                                   int L, uint16_t *__restrict__ M) {
+    __shared__ uint16_t m[32768];
+    const int j0 = blockIdx.x * L, j1 = min(np, j0 + L);
+    if (j0 >= j1) return;
+    for (int j = j0; j < j1; j++) {
         const uint32_t *a = (const uint32_t *)(ta + (uint64_t)slots[j] * 32768);
         const uint32_t *b = (const uint32_t *)(tb + (uint64_t)slots[j] * 32768);
-        uint32_t *d = (uint32_t *)dst;
+        uint32_t nv[16];   // this thread's 32 new entries, two per register
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const uint32_t t = threadIdx.x + 1024u * r;   // 4 entries 4t..4t+3
+            const uint32_t xa = a[t], xb = b[t];
+            uint32_t e[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t v = sym_entry((xa >> (8 * q)) & 255u, (xb >> (8 * q)) & 255u);
+                e[q] = (j == j0 || (v & 0x8000u)) ? v : m[v];
+            }
+            nv[2 * r] = e[0] | (e[1] << 16);
+            nv[2 * r + 1] = e[2] | (e[3] << 16);
+        }
+        __syncthreads();   // every read of the old map is done
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            uint32_t *m32 = (uint32_t *)m;
+            const uint32_t t = threadIdx.x + 1024u * r;
+            m32[2 * t] = nv[2 * r];
+            m32[2 * t + 1] = nv[2 * r + 1];
+        }
+        __syncthreads();
+    }
+    uint32_t *dst = (uint32_t *)(M + (uint64_t)blockIdx.x * 32768);
+    for (uint32_t t = threadIdx.x; t < 16384; t += 1024) dst[t] = ((const uint32_t *)m)[t];
+}
+
+__global__ __launch_bounds__(1024) void ppg_resolve_groups_kernel(const uint16_t *__restrict__ M, int np, int L,
+                                                                  int G, uint8_t *W) {
+    for (int g = 0; g < G; g++) {
+        const int j0 = g * L, j1 = min(np, j0 + L);
+        const uint8_t *src = W + (uint64_t)j0 * 32768;
+        uint32_t *d = (uint32_t *)(W + (uint64_t)j1 * 32768);
+        const uint32_t *mg = (const uint32_t *)(M + (uint64_t)g * 32768);
+        for (uint32_t t = threadIdx.x; t < 8192; t += 1024) {
+            const uint32_t e01 = mg[2 * t], e23 = mg[2 * t + 1];
+            const uint32_t e[4] = {e01 & 0xFFFFu, e01 >> 16, e23 & 0xFFFFu, e23 >> 16};
+            uint32_t v = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) v |= (e[q] & 0x8000u ? e[q] & 255u : (uint32_t)src[e[q]]) << (8 * q);
+            d[t] = v;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(1024) void ppg_resolve_fill_kernel(const uint8_t *__restrict__ ta,
+                                                                const uint8_t *__restrict__ tb,
+                                                                const uint32_t *__restrict__ slots, int np, int L,
+                                                                uint8_t *W) {
+    const int j0 = blockIdx.x * L, j1 = min(np, j0 + L);
+    for (int j = j0; j + 1 < j1; j++) {   // W[j1] came from the groups pass
+        const uint8_t *src = W + (uint64_t)j * 32768;
+        uint32_t *d = (uint32_t *)(W + (uint64_t)(j + 1) * 32768);
+        const uint32_t *a = (const uint32_t *)(ta + (uint64_t)slots[j] * 32768);
+        const uint32_t *b = (const uint32_t *)(tb + (uint64_t)slots[j] * 32768);
         for (uint32_t t = threadIdx.x; t < 8192; t += 1024) {
             const uint32_t xa = a[t], xb = b[t];
             uint32_t v = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const uint32_t x = (xa >> (8 * q)) & 255u, y = (xb >> (8 * q)) & 255u;
-                const uint32_t byte = x == y ? x : src[((((y - x) & 255u) - 1u) << 8) | x];
-                v |= byte << (8 * q);
+                const uint32_t e = sym_entry((xa >> (8 * q)) & 255u, (xb >> (8 * q)) & 255u);
+                v |= (e & 0x8000u ? e & 255u : (uint32_t)src[e]) << (8 * q);
             }
             d[t] = v;
         }
@@ -282,10 +348,20 @@ __global__ __launch_bounds__(1024) void ppg_resolve_kernel(const uint8_t *__rest
     }
 }
 
+// W[1..np] from W[0] (zeroed by the caller); M: scratch of ppg_resolve_groups(np) x 32768 u16
+int ppg_resolve_groups(int np) {
+    int g = 1;
+    while ((int64_t)g * g < np) g++;
+    return g;
+}
+
 hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
-                              uint8_t *W) {
+                              uint8_t *W, uint16_t *M) {
     if (np <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_resolve_kernel, dim3(1), dim3(1024), 0, s, ta, tb, slots, np, W);
+    const int G0 = ppg_resolve_groups(np), L = (np + G0 - 1) / G0, G = (np + L - 1) / L;
+    hipLaunchKernelGGL(ppg_resolve_compose_kernel, dim3(G), dim3(1024), 0, s, ta, tb, slots, np, L, M);
+    hipLaunchKernelGGL(ppg_resolve_groups_kernel, dim3(1), dim3(1024), 0, s, M, np, L, G, W);
+    hipLaunchKernelGGL(ppg_resolve_fill_kernel, dim3(G), dim3(1024), 0, s, ta, tb, slots, np, L, W);
     return hipGetLastError();
 }
 

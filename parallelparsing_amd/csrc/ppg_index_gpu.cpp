@@ -52,7 +52,8 @@ hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *d
                              const uint8_t *ref, uint32_t *diff, int n);
 hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan *spans, PpgAtStats *st, int n);
 hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
-                              uint8_t *W);
+                              uint8_t *W, uint16_t *M);
+int ppg_resolve_groups(int np);
 hipError_t ppg_launch_crc(hipStream_t s, const uint8_t *out, uint64_t n, uint64_t pad, const uint32_t *tabs,
                           uint32_t *seg_raw, uint64_t nseg);
 hipError_t ppg_launch_pack_blocks(hipStream_t s, const PpgBlockEnd *blk, const PpgInflateJob *jobs,
@@ -263,7 +264,9 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     hipStream_t s = B.s;
     const uint64_t d0 = 8ull * (uint64_t)hl;
     const uint64_t end_bits = 8ull * (uint64_t)(len - 8);   // no block header starts in the trailer
-    if (piece_bytes <= 0) piece_bytes = std::min<int64_t>(4 << 20, std::max<int64_t>(256 << 10, len / 16384));
+    // default ~65k pieces (768 KiB for a 50 GB member: 3.41 s vs 3.72 s at 16k pieces, r02 --ix-piece-kib
+    // sweep -- pass 2's batches hold several generations of waves; smaller pieces cost more setup)
+    if (piece_bytes <= 0) piece_bytes = std::min<int64_t>(4 << 20, std::max<int64_t>(256 << 10, len / 65536));
     const uint64_t pbits = 8ull * (uint64_t)piece_bytes;
 
     // ---- 1. candidate block starts ----
@@ -455,11 +458,18 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         std::vector<uint32_t> sl(np);
         for (size_t j = 0; j < np; j++) sl[j] = real[j].slot;
         DevBuf<uint32_t> dsl;
+        DevBuf<uint16_t> maps;          // composed per-group maps
         HIPCHK(dsl.alloc(np));
+        HIPCHK(maps.alloc((size_t)ppg_resolve_groups((int)np) * kWin));
         HIPCHK(hipMemcpyAsync(dsl.p, sl.data(), 4 * np, hipMemcpyHostToDevice, s));
-        HIPCHK(ppg_launch_resolve(s, B.ta.p, B.tb.p, dsl.p, (int)np, W.p));
+        HIPCHK(ppg_launch_resolve(s, B.ta.p, B.tb.p, dsl.p, (int)np, W.p, maps.p));
         HIPCHK(hipStreamSynchronize(s));
     }
+    // pass 1's device state is spent (block lists live on the host): ~190 KiB per slot
+    for (DevBuf<uint8_t> *b : {&B.ring, &B.ta, &B.tb}) b->release();
+    B.blk.release();
+    B.bigblk.release();
+    B.dense.release();
     stat[9] = ms_since(t);
 
     // ---- 4. pass 2: exact output, batch by batch ----
