@@ -6,6 +6,9 @@
 #include <stdio.h>
 #include <string.h>
 #include <vector>
+#include <memory>
+#include <new>
+#include <utility>
 #include <algorithm>
 
 #include "../../include/ppgpu.h"
@@ -35,21 +38,46 @@ struct PpgPoint {                       // Common/Index.cs:51-82
     std::vector<uint8_t> offset;        // bytes since the last '@' (the partial record)
 };
 
+// allocator whose value-initialisation is default-initialisation: resize() leaves bytes
+// uninitialised, so a window array can grow and be filled by one device-to-host copy
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U> &) {}
+    template <class U>
+    void construct(U *p) noexcept { ::new ((void *)p) U; }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
+};
+using ByteVec = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
+
 struct ppg_index {
     int32_t chunk_max_bytes = 0;
     std::vector<PpgPoint> pts;
     // Point.Window (the preceding 32 KiB of output, oldest first) of point i at i * kWin: one
     // contiguous array, so a range of chunks ships its windows to the GPU in one copy
-    std::vector<uint8_t> windows;
+    ByteVec windows;
     const uint8_t *win(size_t i) const { return windows.data() + i * kWin; }
     // side points (ppg_index_build_gpu_side; not part of the .gzi): block starts inside chunks,
     // absolute bit / output and their 32 KiB windows, for ppg_shard_set_split
     std::vector<int64_t> side_bit, side_out;
-    std::vector<uint8_t> side_win;
+    ByteVec side_win;
 
     // Index.AddPoint (Common/Index.cs:24-48)
     void add_point(int bits, int64_t input, int64_t output, uint32_t left, const uint8_t *circ,
                    const uint8_t *off, size_t off_len) {
+        // oldest bytes (those after the circular write head) first
+        windows.insert(windows.end(), circ + (kWin - left), circ + kWin);
+        windows.insert(windows.end(), circ, circ + (kWin - left));
+        add_point_fields(bits, input, output, off, off_len);
+    }
+    // the same without the window (the caller has appended it to `windows` already)
+    void add_point_fields(int bits, int64_t input, int64_t output, const uint8_t *off, size_t off_len) {
         if (pts.empty()) {
             chunk_max_bytes = (int32_t)output;
         } else {
@@ -60,9 +88,6 @@ struct ppg_index {
         p.output = output;
         p.input = input;
         p.bits = bits;
-        // oldest bytes (those after the circular write head) first
-        windows.insert(windows.end(), circ + (kWin - left), circ + kWin);
-        windows.insert(windows.end(), circ, circ + (kWin - left));
         p.offset.assign(off, off + off_len);
         pts.push_back(std::move(p));
     }

@@ -645,17 +645,13 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             }
         }
         nblocks_seen += refs.size();
-        // windows of the picked Points (zero-output Points keep the all-zero window)
+        // windows of the picked Points, then the side points', gathered on the device in index order
+        // and copied straight onto the index's window arrays (a zero-output Point reads W[0]: zeros)
         std::vector<PpgGather> gw;
         for (const Pick &p : picks)
-            if (p.output > 0) gw.push_back(PpgGather{h2[p.j].out_off, (uint64_t)p.j * kWin, p.rel, ~0ull, 0});
-        const size_t npick_w = gw.size();
+            gw.push_back(p.output > 0 ? PpgGather{h2[p.j].out_off, (uint64_t)p.j * kWin, p.rel, ~0ull, 0}
+                                      : PpgGather{0, 0, 0, ~0ull, 0});
         for (const Side &d : sides) gw.push_back(PpgGather{h2[d.j].out_off, (uint64_t)d.j * kWin, d.rel, ~0ull, 0});
-        // host staging of the gathered windows: uninitialised (a zero-filled vector of ~1.7 GB per
-        // 50 GB member costs a memset), and the index's window array grows once per batch
-        const size_t hw_n = gw.size() * kWin;
-        std::unique_ptr<uint8_t[]> hw_buf(new uint8_t[std::max<size_t>(hw_n, 1)]);
-        uint8_t *const hw = hw_buf.get();
         // grown to the whole member's projected size (at least x1.5): an exact per-batch reserve
         // recopied every window so far on every batch (quadratic in the batch count)
         const double proj = 1.02 * (double)total / (double)std::max<uint64_t>(O[b1], 1);
@@ -664,28 +660,32 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         grow(ix.side_bit, ix.side_bit.size() + sides.size(), proj);
         grow(ix.side_out, ix.side_out.size() + sides.size(), proj);
         grow(ix.side_win, ix.side_win.size() + sides.size() * kWin, proj);
+        const size_t w0 = ix.windows.size(), s0 = ix.side_win.size();
+        ix.windows.resize(w0 + picks.size() * kWin);          // uninitialised (ByteVec)
+        ix.side_win.resize(s0 + sides.size() * kWin);
         if (!gw.empty()) {
             HIPCHK(B.gat.alloc(gw.size()));
             HIPCHK(dwin.alloc(gw.size() * kWin));
             HIPCHK(hipMemcpyAsync(B.gat.p, gw.data(), sizeof(PpgGather) * gw.size(), hipMemcpyHostToDevice, s));
             HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, dwin.p, nullptr, nullptr, (int)gw.size()));
-            HIPCHK(hipMemcpyAsync(hw, dwin.p, hw_n, hipMemcpyDeviceToHost, s));
+            if (!picks.empty())
+                HIPCHK(hipMemcpyAsync(ix.windows.data() + w0, dwin.p, picks.size() * kWin, hipMemcpyDeviceToHost, s));
+            if (!sides.empty())
+                HIPCHK(hipMemcpyAsync(ix.side_win.data() + s0, dwin.p + picks.size() * kWin, sides.size() * kWin,
+                                      hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
-        for (size_t i = 0; i < sides.size(); i++) {
-            ix.side_bit.push_back((int64_t)sides[i].end_bit);
-            ix.side_out.push_back(sides[i].output);
-            const uint8_t *w = hw + (npick_w + i) * kWin;
-            ix.side_win.insert(ix.side_win.end(), w, w + kWin);
+        for (const Side &d : sides) {
+            ix.side_bit.push_back((int64_t)d.end_bit);
+            ix.side_out.push_back(d.output);
         }
-        size_t wi = 0;
-        for (const Pick &p : picks) {
-            if (p.output == 0) {
-                ix.add_point((int)p.bits, p.input, 0, 0, zeros.data(), nullptr, 0);
-            } else {
-                const uint8_t *w = hw + (wi++) * kWin;
-                ix.add_point((int)p.bits, p.input, p.output, 0, w, w + kWin - p.off_len, (size_t)p.off_len);
-            }
+        for (size_t i = 0; i < picks.size(); i++) {
+            const Pick &p = picks[i];
+            const uint8_t *w = ix.windows.data() + w0 + i * kWin;
+            if (p.output == 0)
+                ix.add_point_fields((int)p.bits, p.input, 0, nullptr, 0);
+            else
+                ix.add_point_fields((int)p.bits, p.input, p.output, w + kWin - p.off_len, (size_t)p.off_len);
         }
         t_census += ms_since(tc);
         b0 = b1;
