@@ -147,7 +147,7 @@ def pmc_traffic(workload, launches_per_step):
     return t.get("hbm_bytes_per_launch")
 
 
-def ingest_run(tf, ix, dev, threads):
+def ingest_run(tf, ix, dev, threads, piece_gib=8.0):
     """Host-ingest path (ppg_file_decompress_all): the same member written to $TMPDIR as a real
     file, streamed from page cache through pinned buffers, PCIe and the kernels."""
     import parallelparsing_amd as pp
@@ -158,13 +158,14 @@ def ingest_run(tf, ix, dev, threads):
             for lo in range(0, tf.file_len, 1 << 30):
                 f.write(tf.file_bytes(lo, min(tf.file_len, lo + (1 << 30))))
         wt = time.perf_counter() - t
-        pp.decompress_file(ix, path, device=dev, threads=threads)   # warm: buffers, page cache
-        _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=threads)
+        pb = int(piece_gib * (1 << 30))
+        pp.decompress_file(ix, path, device=dev, threads=threads, piece_bytes=pb)   # warm: buffers, page cache
+        _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=threads, piece_bytes=pb)
         assert tot == tf.expected_records(), (tot, tf.expected_records())
         return {"records_per_s": tot / sec, "compressed_GBps": tf.file_len / sec / 1e9,
                 "decompressed_GBps": tf.text_len * tf.repeats / sec / 1e9, "seconds": sec,
                 "file_GB": tf.file_len / 1e9, "write_s": wt,
-                "note": f"file in page cache -> pread ({threads} threads) -> pinned -> H2D -> decode, 8 GiB pieces "
+                "note": f"file in page cache -> pread ({threads} threads) -> pinned -> H2D -> decode, {piece_gib:g} GiB pieces "
                         "(three device slots, per-slot streams: a piece's decode overlaps the previous one's tail); "
                         "PCIe-inclusive, not the bench value"}
     finally:
@@ -467,6 +468,8 @@ def main():
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ingest-piece-gib", type=float, default=8,
+                    help="ingest leg: compressed GiB per pipelined piece (ppg_file_decompress_all piece_bytes)")
     ap.add_argument("--ix-piece-kib", type=float, default=0,
                     help="--create-index: compressed bytes per pass-1 piece in KiB (0 = the library's default)")
     ap.add_argument("--ix-capacity-gib", type=float, default=0,
@@ -693,7 +696,7 @@ def main():
         line["create_index"] = create_index_run(tf, args, dev)
     if rank == 0 and world == 1 and args.ingest:
         try:
-            line["ingest"] = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads)
+            line["ingest"] = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads, args.ingest_piece_gib)
         except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
             line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
