@@ -42,19 +42,57 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_input(args):
+def shared_tiled(args, key, build):
+    """The synthetic member, built once per node: at N = 1 in this process; at N > 1 local rank 0
+    builds it and saves it under /dev/shm (TiledFile.save), the other ranks memory-map that copy
+    (TiledFile.load) instead of each rebuilding the ~4 GB text segment and deflating it (22 s and
+    ~5 GB of host RAM per rank, VERDICT r02 weak #4).  Returns (TiledFile, seconds, how)."""
     from parallelparsing_amd.tiled import TiledFile
     t = time.time()
+    if args.world == 1:
+        return build(), time.time() - t, "built"
+    job = os.environ.get("TORCHELASTIC_RUN_ID", "") + "_" + os.environ.get("MASTER_PORT", "")
+    import hashlib   # (str hashes are salted per process: every rank must derive the same name)
+    d = os.path.join(args.shm_dir, "ppg_bench_" + hashlib.sha1(repr((job, key)).encode()).hexdigest()[:12])
+    args.shm_paths.append(d)
+    if args.local_rank == 0:
+        tf = build()
+        tf.save(d)
+        return tf, time.time() - t, f"built (shared via {d})"
+    ready = os.path.join(d, "ready")
+    while not os.path.exists(ready):
+        if time.time() - t > 1800:
+            raise TimeoutError(f"local rank 0 did not publish {d}")
+        time.sleep(0.2)
+    return TiledFile.load(d), time.time() - t, f"memory-mapped from {d}"
+
+
+def drop_shared(args):
+    """After every rank has loaded it (a barrier): local rank 0 removes the /dev/shm copy (the
+    ranks' mappings stay valid)."""
+    import shutil
+    if args.local_rank == 0:
+        for d in args.shm_paths:
+            shutil.rmtree(d, ignore_errors=True)
+
+
+def build_input(args):
+    from parallelparsing_amd.tiled import TiledFile
     if args.workload == "50gb":
         # weak scaling: the member holds `repeats` segments per rank (~50 GB of gzip per GPU)
         # weak (default): ~50 GB of gzip per GPU; strong: one ~50 GB member split over the GPUs
         # (BASELINE configs[3] literally)
         reps = args.repeats * (args.world if args.scaling == "weak" else 1)
-        tf = TiledFile(args.seg_records, reps, args.chunk, threads=args.host_threads, blank_lines=args.blank_lines)
+        key = ("50gb", args.seg_records, reps, args.chunk, args.blank_lines)
+        build = lambda: TiledFile(args.seg_records, reps, args.chunk, threads=args.host_threads,   # noqa: E731
+                                  blank_lines=args.blank_lines)
     else:  # 1m: configs[1], one non-repeated 1 M-read member
-        tf = TiledFile(1_000_000, 1, args.chunk, threads=args.host_threads)
+        key = ("1m", args.chunk)
+        build = lambda: TiledFile(1_000_000, 1, args.chunk, threads=args.host_threads)   # noqa: E731
+    tf, sec, how = shared_tiled(args, key, build)
+    args.input_seconds, args.input_how = sec, how
     log(f"[bench] input: {tf.records * tf.repeats:,} records, {tf.text_len * tf.repeats / 1e9:.1f} GB text, "
-        f"{tf.file_len / 1e9:.2f} GB gz, {tf.npoints - 1} chunks, built in {time.time() - t:.1f}s")
+        f"{tf.file_len / 1e9:.2f} GB gz, {tf.npoints - 1} chunks, {how} in {sec:.1f}s")
     return tf
 
 
@@ -133,16 +171,18 @@ def cpu_baseline(tf, ix_out, ix_in, nchunks, threads):
             "decompressed_MBps": out_bytes / dt / 1e6, "variants": variants}
 
 
-def pmc_traffic(workload, launches_per_step):
+def pmc_traffic(workload, build, path=None):
     """HBM bytes per inflate launch from the committed rocprofv3 PMC passes of this same command
-    (profiles/traffic.json, written by the profiling recipe in DESIGN.md), or None."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    (profiles/traffic.json, written by tools/profile_round.sh + tools/traffic_summary.py), or None.
+    The file names the workload and the library build it measured (ppg_version + ppg_build_id, a
+    hash of the inflate object): counters of another build or workload are never quoted."""
+    path = path or os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("workload") != workload:
+    if t.get("workload") != workload or t.get("build") != build:
         return None
     return t.get("hbm_bytes_per_launch")
 
@@ -243,47 +283,74 @@ def paired_run(args, dev, world=1, rank=0, xdev=None):
     files (dist.partition_chunks per file); the files' record ranges do not line up across ranks,
     so the pair check is a real exchange: paired.distributed_pair_check all-gathers the counts and
     moves every spot key to the rank owning its pair number (all_to_all, RCCL over xGMI).  Size per
-    file: --paired-repeats segments (default: ~12.5 GB of gzip per file on one GPU -- both decoded
-    outputs must stay resident for pairing -- and configs[4]'s 25 GB per file for N > 1)."""
+    file: --paired-repeats segments (default 102: configs[4]'s ~25 GB of gzip per file at any N).
+    The spot keys are extracted per output batch while it is resident (ppg_shard_set_keys), so a
+    rank's range may decode in several batches of --paired-out-gib: on one GPU the two ~103 GB
+    outputs never need to be resident together."""
     import torch
     import parallelparsing_amd as pp
     from parallelparsing_amd import paired
     from parallelparsing_amd.dist import partition_chunks
     from parallelparsing_amd.tiled import TiledFile
-    reps = args.paired_repeats or (51 if world == 1 else 102)
+    reps = args.paired_repeats or 102
     t = time.time()
-    tfs = [TiledFile(args.seg_records, reps, 50_000, seed=m - 1, mate=m, threads=args.host_threads)
+    tfs = [shared_tiled(args, ("paired", args.seg_records, reps, m),
+                        lambda m=m: TiledFile(args.seg_records, reps, 50_000, seed=m - 1, mate=m,
+                                              threads=args.host_threads))[0]
            for m in (1, 2)]
+    args.input_seconds = time.time() - t
     log(f"[bench] paired input: 2 x {tfs[0].records * tfs[0].repeats:,} records, "
-        f"{tfs[0].file_len / 1e9:.2f} + {tfs[1].file_len / 1e9:.2f} GB gz, built in {time.time() - t:.1f}s")
+        f"{tfs[0].file_len / 1e9:.2f} + {tfs[1].file_len / 1e9:.2f} GB gz, ready in {args.input_seconds:.1f}s")
     # one ctx (= one HIP stream) per file, so the two DecompressAll passes run concurrently: at
     # chunk = 50,000 one file has only ~2.7k chunks, a third of the GPU's 8k wave slots
     ctxs = [pp.Device(dev.index), pp.Device(dev.index)]
     ranges = [partition_chunks(tf.p_input, world)[rank] for tf in tfs]
     args.split, _ = auto_split(args, wave_slots(dev), sum(b - a for a, b in ranges))
     shards, bufs = [], []
+    t_setup = time.time()
     for tf, ctx, (a, b) in zip(tfs, ctxs, ranges):
         lo, hi = int(tf.p_input[a]) - 1, int(tf.p_input[b])
         comp = torch.empty(hi - lo + 256, dtype=torch.uint8, device=dev)
         comp[hi - lo:].zero_()
         tf.fill_device(comp, lo, hi)
         bufs.append(comp)
-        out_cap = int(tf.p_output[b] - tf.p_output[a]) + (1 << 20)
-        shards.append(pp.Shard(tf.index(a, b + 1), comp.data_ptr(), first=0, n=b - a, device=ctx,
-                               comp_on_device=True, comp_len=hi - lo, out_capacity=out_cap))
+        text = int(tf.p_output[b] - tf.p_output[a])
+        out_cap = min(text + (1 << 20), int(args.paired_out_gib * (1 << 30)))
+        sh = pp.Shard(tf.index(a, b + 1), comp.data_ptr(), first=0, n=b - a, device=ctx,
+                      comp_on_device=True, comp_len=hi - lo, out_capacity=out_cap)
+        # keys per output batch, into a buffer sized for >= 200-B records (the run fails loudly,
+        # PPG_BUF_ERROR, if a file has more)
+        paired.attach_keys(sh, text // 200 + 4096)
         if args.split > 1:
-            shards[-1].set_split(*tf.side_points(a, b + 1, args.split))
+            sh.set_split(*tf.side_points(a, b + 1, args.split))
+        shards.append(sh)
     torch.cuda.synchronize()
-    log(f"[bench] rank {rank}: R1 chunks [{ranges[0][0]},{ranges[0][1]}), R2 chunks [{ranges[1][0]},{ranges[1][1]})")
+    setup_s = time.time() - t_setup
+    log(f"[bench] rank {rank}: R1 chunks [{ranges[0][0]},{ranges[0][1]}), R2 chunks [{ranges[1][0]},{ranges[1][1]}), "
+        f"{shards[0].batches} + {shards[1].batches} output batches, setup {setup_s:.1f}s")
 
     import threading
 
     def step():
-        th = [threading.Thread(target=sh.run) for sh in shards]   # ctypes drops the GIL
+        errs = []
+
+        def run(sh):
+            try:
+                sh.run()
+            except pp.PpgError as e:   # raised below, after the threads (and, N > 1, the other ranks) meet
+                errs.append(e)
+        th = [threading.Thread(target=run, args=(sh,)) for sh in shards]   # ctypes drops the GIL
         for x in th:
             x.start()
         for x in th:
             x.join()
+        if world > 1:   # a failing rank must not leave the others in the key exchange
+            f = torch.tensor([len(errs)], dtype=torch.int64, device=xdev)
+            dist.all_reduce(f)
+            if int(f.item()):
+                raise errs[0] if errs else RuntimeError("DecompressAll failed on another rank")
+        elif errs:
+            raise errs[0]
         keys = [paired.dedup(paired.shard_keys(sh))[0] for sh in shards]
         if world == 1:
             return paired.check_pairs(keys[0], keys[1])
@@ -327,9 +394,12 @@ def paired_run(args, dev, world=1, rank=0, xdev=None):
         "config": {"workload": f"configs[4]-shaped: 2 x {tfs[0].file_len / 1e9:.1f} GB .fastq.gz over {world} GPU(s), "
                                f"chunk=50000, pair chunks of 50,000 records",
                    "pairs": npairs, "gz_bytes": [tf.file_len for tf in tfs], "decompressed_bytes": text,
+                   "output_batches_per_file": [sh.batches for sh in shards],
+                   "keys": "per output batch while resident (ppg_shard_set_keys)",
                    "pair_check": "on-device" if world == 1 else "all_to_all of spot keys to pair owners",
                    "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
         "decompressed_MBps": text * args.steps / elapsed / 1e6,
+        "setup_s": {"input": round(args.input_seconds, 2), "shards": round(setup_s, 2)},
     }
 
 
@@ -442,7 +512,8 @@ def rccl_info(world, backend):
     import torch
     import torch.distributed as dist
     import parallelparsing_amd as pp
-    info = {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None,
+    on = dist.is_available() and dist.is_initialized()
+    info = {"world_size": dist.get_world_size() if on else 1, "backend": backend if on else None,
             "libppgpu_rccl_version": pp.rccl_version()}
     try:
         info["rccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
@@ -467,6 +538,8 @@ def main():
                          "GPUs; weak: ~50 GB of gzip per GPU")
     ap.add_argument("--out-capacity-gib", type=float, default=192.0)   # one batch: 50 GB gz + 192 GiB out fit 288 GB
     ap.add_argument("--host-threads", type=int, default=16)
+    ap.add_argument("--shm-dir", default="/dev/shm",
+                    help="N > 1: where local rank 0 publishes the built input member for the other ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ingest-piece-gib", type=float, default=8,
                     help="ingest leg: compressed GiB per pipelined piece (ppg_file_decompress_all piece_bytes)")
@@ -478,7 +551,10 @@ def main():
                     help="also time the GPU CreateIndex over the whole member (reported under 'create_index')")
     ap.add_argument("--paired", action="store_true",
                     help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
-    ap.add_argument("--paired-repeats", type=int, default=0)   # 0: 51 (~12.5 GB gz per file) on 1 GPU, 102 for N > 1
+    ap.add_argument("--paired-repeats", type=int, default=0)   # 0: 102 (configs[4]: ~25 GB gz per file)
+    ap.add_argument("--paired-out-gib", type=float, default=56.0,
+                    help="--paired: output buffer per file in GiB (a rank's range decodes in batches of this; the "
+                         "spot keys are extracted per batch)")
     ap.add_argument("--tail2", default="16:0.25",
                     help="S2:G2 -- of the split chunks, the last G2 generations into up to S2 waves each "
                          "(default 16:0.25; off = none)")
@@ -516,6 +592,10 @@ def main():
         args.scaling = "strong" if world > 1 else "weak"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    args.local_rank, args.shm_paths = local, []
+    # PPG_BENCH_FORCE_DIST=1 (tests): the N > 1 glue -- process group, the library's RCCL
+    # communicator from a broadcast unique id, the count all-gather -- even at world size 1
+    dist_on = world > 1 or os.environ.get("PPG_BENCH_FORCE_DIST") == "1"
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     if os.environ.get("PPG_BENCH_DRYRUN"):   # launcher test (tests/test_bench_launch.py): no GPU
@@ -531,7 +611,7 @@ def main():
     backend = os.environ.get("PPG_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if dist_on:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
@@ -547,7 +627,9 @@ def main():
         line["communicator"] = rccl_info(world, backend)
         if rank == 0:
             print(json.dumps(line), flush=True)
-        if world > 1:
+        if dist_on:
+            dist.barrier()
+            drop_shared(args)
             dist.destroy_process_group()
         return
 
@@ -563,6 +645,7 @@ def main():
     lo, hi = int(ix_in[a]) - 1, int(ix_in[b])   # file bytes [Input_a - 1, Input_b - 1]
     comp_len = hi - lo
     t = time.time()
+    t_setup = time.time()
     comp = torch.empty(comp_len + 256, dtype=torch.uint8, device=dev)
     comp[comp_len:].zero_()
     tf.fill_device(comp, lo, hi)
@@ -580,25 +663,47 @@ def main():
     args.split_chunks = ksplit if args.split > 1 else 0
     args.tail2_s, args.tail2_k = tail2_split(args, wave_slots(dev), ksplit) if args.split > 1 else (1, 0)
     n_side = int(sb.size) if args.split > 1 else 0
+    setup_s = time.time() - t_setup
     log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
-        f"{shard.batches} output batch(es), setup {time.time() - t:.1f}s")
+        f"{shard.batches} output batch(es), setup {setup_s:.1f}s")
     counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
-    comm, gather_via = (None, None) if world == 1 else make_comm(ctx, world, rank, backend, xdev)
+    comm, gather_via = (None, None) if not dist_on else make_comm(ctx, world, rank, backend, xdev)
     bounds = np.array([r[0] for r in ranges] + [ranges[-1][1]], np.int32)
+    # per-rank setup seconds (input ready, shard ready) of every rank, in the line
+    setup = torch.tensor([args.input_seconds, setup_s], dtype=torch.float64, device=xdev)
+    if dist_on:
+        allset = torch.zeros(world, 2, dtype=torch.float64, device=xdev)
+        dist.all_gather_into_tensor(allset, setup)
+        setup_ranks = allset.cpu().tolist()
+        drop_shared(args)   # every rank has mapped the shared input by now
+    else:
+        setup_ranks = [setup.tolist()]
 
     def step():
-        shard.run()
-        if world > 1:
-            if comm is not None:   # the C ABI's count all-gather (ppg_shard_gather_counts)
+        err = None
+        try:
+            shard.run()
+        except pp.PpgError as e:
+            err = e
+        if dist_on:
+            if comm is not None:
+                # the C ABI's count all-gather (ppg_shard_gather_counts): a rank whose run failed
+                # still joins, and every rank raises the first failing rank's status
                 c, bs, _ = pp.gather_counts(shard, comm, bounds)
                 return c, bs
+            f = torch.tensor([1 if err else 0], dtype=torch.int64, device=xdev)
+            dist.all_reduce(f)   # the torch fallback: agree on failure before the gather
+            if int(f.item()):
+                raise err or RuntimeError("DecompressAll failed on another rank")
             shard.counts_to_device(counts_dev.data_ptr())
             return gather_counts(counts_dev[: b - a].to(xdev), ranges, device=xdev)
+        if err:
+            raise err
         return None
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -609,10 +714,10 @@ def main():
         infl_ms += tm["inflate_ms"]
         parse_ms += tm["parse_ms"]
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -622,7 +727,7 @@ def main():
     assert (r["status"] == 0).all(), "chunk errors"
     assert (r["produced"] == (ix_out[a + 1:b + 1] - ix_out[a:b])).all(), "produced != to.Output - from.Output"
     local_records = int(r["records"].sum())
-    if world > 1:
+    if dist_on:
         counts, bases = g
         total_records = int(counts.sum())
     else:
@@ -631,7 +736,8 @@ def main():
     if args.share > 1:
         expect = None   # a share: produced lengths and statuses are checked above, counts per range below
         line_share = {"share_of": args.share, "chunks": [a, b], "records": total_records}
-    if expect is not None and not os.environ.get("PPG_PROBE_NO_CENSUS"):   # an A/B probe produces no records
+    if expect is not None and not (os.environ.get("PPG_PROBE_NO_CENSUS") or os.environ.get("PPG_PROBE")):
+        # (an A/B timing probe: no records, or wrong bytes by design)
         assert total_records == expect, (total_records, expect)
 
     text_bytes = int(ix_out[-1] - ix_out[0])
@@ -645,6 +751,7 @@ def main():
     workload = ("configs[1]: 1 M-read .fastq.gz, chunk=10000" if args.workload != "50gb"
                 else "configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000" if args.scaling == "weak" or world == 1
                 else f"configs[3]: ~50 GB .fastq.gz sharded across {world} GPUs, chunk=10000")
+    build = pp.build_info()
     line = {
         "metric": "FASTQ records/sec + decompressed MB/s, 50 GB .fastq.gz, 1/2/4/8 MI355X",
         "value": rec_s,
@@ -669,14 +776,14 @@ def main():
         "decompressed_MBps": text_bytes * args.steps / elapsed / 1e6,
         "kernel_ms_per_step": {"inflate": infl_ms / args.steps, "parse": parse_ms / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload, shard.batches),
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload, build),
                      "kernel": "ppg_inflate_kernel", "alg_bytes_per_launch": alg_local / shard.batches,
                      "mean_launch_ms": mean_launch_s * 1e3,
                      # memory-side bytes (2 x FETCH_SIZE + WRITE_SIZE, calibrated, Infinity-Cache hits
                      # included) over the same launch time: how much of the HBM peak the traffic is
                      **({"traffic_GBps": traffic / mean_launch_s / 1e9,
                          "traffic_frac": traffic / mean_launch_s / 1e9 / HBM_PEAK_GBS}
-                        if (traffic := pmc_traffic(workload, shard.batches)) else {}),
+                        if (traffic := pmc_traffic(workload, build)) else {}),
                      # SURVEY §8d's secondary terms (not in alg_bytes), per launch of this rank
                      "secondary_bytes_per_launch": {
                          "windows": 32768 * (b - a + n_side) // shard.batches,
@@ -687,6 +794,11 @@ def main():
         "reference_published_rec_s": REFERENCE_REC_S,
         **({"rehearsal_share": line_share} if args.share > 1 else {}),
         "communicator": dict(rccl_info(world, backend), count_gather=gather_via),
+        "build": build,
+        # seconds per rank before timing: the input member ready (built once per node, shared via
+        # /dev/shm for N > 1), then the rank's shard resident in HBM (compressed range, windows)
+        "setup_s": {"input_how": args.input_how, "per_rank": [{"input": round(x, 2), "shard": round(y, 2)}
+                                                               for x, y in setup_ranks]},
     }
     args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines and args.share == 1
     if rank == 0 and world == 1 and (args.ingest or args.create_index):
@@ -705,7 +817,7 @@ def main():
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

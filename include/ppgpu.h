@@ -178,7 +178,9 @@ int ppg_shard_results(ppg_shard *sh, int64_t *records, int64_t *produced, int32_
 int64_t ppg_shard_total_records(ppg_shard *sh);
 int32_t ppg_shard_batches(ppg_shard *sh);
 
-/* Valid only when the shard ran as one batch: chunk bytes / record descriptors to the host.
+/* Chunk bytes (only when the shard ran as one batch: the output buffer is reused by the next
+ * batch; ppg_cursor streams bytes of any size) / record descriptors (any number of batches: the
+ * descriptors of every batch stay resident) to the host.
  * Descriptor j of chunk k = 4 uint32 (n1,n2,n3,n4) relative to raw_k = offset_k ++ chunk_k:
  * Identifier=[r+1,n1) Sequence=[n1+1,n2) Other=[n2+2,n3) Quality=[n3+1,n4), where r = 0 for
  * the chunk's first record and the previous n4+1 otherwise (Parsing.cs:11-51). */
@@ -195,6 +197,11 @@ int ppg_shard_copy_output(ppg_shard *sh, int64_t off, int64_t len, void *dst, in
  * the digits between the first two '.' of the Identifier ("SRR<id>.<spot>.<mate> ..."), -1 when
  * absent, -2 for a record the reference parses twice, which a pairing drops. */
 int ppg_shard_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap);
+/* The same keys for a shard of any number of batches: from the next ppg_shard_run on, each batch
+ * writes its records' keys to dev_keys[shard record number] (caller device memory on this GPU, cap
+ * entries) on the ctx stream while its output is resident.  NULL / 0 turns it off.  A run with
+ * more records than cap fails with PPG_BUF_ERROR. */
+int ppg_shard_set_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap);
 
 /* Device-resident per-chunk record counts (int64[n]) copied to caller device memory on this
  * GPU (the input of the cross-GPU all-gather). */
@@ -286,6 +293,10 @@ int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, c
 
 /* Library build string (kernel ISA, version). */
 const char *ppg_version(void);
+/* "inflate-<16 hex>": a hash of the inflate kernels' object (all variants + launcher), fixed at
+ * build time.  Measurements quoted from files (bench.py's roofline.traffic) carry it and are
+ * refused when it differs from the library in use. */
+const char *ppg_build_id(void);
 
 #ifdef __cplusplus
 }

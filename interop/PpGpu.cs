@@ -90,6 +90,7 @@ internal static unsafe class PpGpu
     [DllImport(Lib)] public static extern int ppg_shard_copy_output(nint shard, long off, long len, void* dst,
         int dstOnDevice);
     [DllImport(Lib)] public static extern int ppg_shard_keys(nint shard, long* devKeys, long cap);
+    [DllImport(Lib)] public static extern int ppg_shard_set_keys(nint shard, long* devKeys, long cap);
     [DllImport(Lib)] public static extern int ppg_shard_counts_to_device(nint shard, long* devDst);
     [DllImport(Lib)] public static extern int ppg_shard_timing(nint shard, out float inflateMs, out float parseMs,
         out float totalMs);
@@ -121,6 +122,7 @@ internal static unsafe class PpGpu
         long outCapacity, long* counts, long* bases, out long totalRecords);
 
     [DllImport(Lib)] public static extern nint ppg_version();
+    [DllImport(Lib)] public static extern nint ppg_build_id();
 
     public static void Check(int rc)
     {

@@ -436,6 +436,21 @@ class Shard:
                                       _ptr(windows) if n else None), "set_split")
         return self
 
+    def set_keys(self, keys):
+        """From the next run on, every output batch writes its records' spot keys (paired reads,
+        ppg_record_keys) into `keys`, an int64 CUDA tensor on this device indexed by shard record
+        number (ppg_shard_set_keys): works for shards of any number of batches.  None turns it off."""
+        if keys is None:
+            check(lib.ppg_shard_set_keys(self._h, None, 0), "set_keys")
+            self._keys = None
+            return self
+        import torch
+        if not (keys.is_cuda and keys.dtype == torch.int64 and keys.is_contiguous()):
+            raise ValueError("set_keys: keys must be a contiguous int64 CUDA tensor")
+        self._keys = keys   # kept alive while the library may write it
+        check(lib.ppg_shard_set_keys(self._h, C.c_void_p(keys.data_ptr()), keys.numel()), "set_keys")
+        return self
+
     def results(self):
         n = self.n
         rec, prod, end = (np.zeros(n, np.int64) for _ in range(3))
@@ -525,6 +540,11 @@ class Comm:
 
     def __del__(self):
         self.close()
+
+
+def build_info():
+    """The library in use: ppg_version() and ppg_build_id() (a hash of the inflate kernels' object)."""
+    return {"ppg_version": lib.ppg_version().decode(), "build_id": lib.ppg_build_id().decode()}
 
 
 def rccl_version():

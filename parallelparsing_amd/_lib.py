@@ -101,10 +101,12 @@ _SIGS = {
     "ppg_shard_record_base": (C.c_int, [vp, vp]),
     "ppg_shard_copy_output": (C.c_int, [vp, i64, i64, vp, C.c_int]),
     "ppg_shard_keys": (C.c_int, [vp, vp, i64]),
+    "ppg_shard_set_keys": (C.c_int, [vp, vp, i64]),
     "ppg_shard_counts_to_device": (C.c_int, [vp, vp]),
     "ppg_shard_timing": (C.c_int, [vp, P(C.c_float), P(C.c_float), P(C.c_float)]),
     "ppg_file_decompress_all": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, vp, P(i64), P(C.c_double)]),
     "ppg_version": (C.c_char_p, []),
+    "ppg_build_id": (C.c_char_p, []),
     "ppg_cursor_open": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, P(vp)]),
     "ppg_cursor_next": (C.c_int, [vp, vp]),
     "ppg_cursor_batches": (i32, [vp]),

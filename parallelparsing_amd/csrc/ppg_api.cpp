@@ -315,7 +315,7 @@ int ppg_index_validate(const ppg_index *ix, int32_t first, int32_t n) {
     return PPG_OK;
 }
 
-const char *ppg_version(void) { return "ppgpu 0.1 gfx950 (wave-per-chunk inflate, LDS 32 KiB ring)"; }
+const char *ppg_version(void) { return "ppgpu 0.3 gfx950 (wave-per-chunk inflate, 1 KiB LDS history ring, fused newline census)"; }
 
 }  // extern "C"
 
@@ -521,9 +521,10 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
     if ((size_t)out_cap + 64 > sh->out.n) HIPCHK(sh->out.alloc((size_t)out_cap + 64));
     sh->out_cap = (int64_t)sh->out.n - 64;
     HIPCHK(hipMemsetAsync(sh->out.p + out_cap, 0, 64, s));
-    // descriptor space (16 B per record) sized for >= 256-B records; a batch that needs more
-    // grows it before its emit pass (ppg_shard_run)
-    HIPCHK(sh->recs.alloc((size_t)(4 * (out_cap / 256 + 1024))));
+    // descriptor space (16 B per record) for every record of the shard (all batches: copy_records
+    // and the keys stay valid for multi-batch shards) sized for >= 256-B records; a batch that needs
+    // more grows it, keeping the earlier batches' descriptors (batch_collect)
+    HIPCHK(sh->recs.alloc((size_t)(4 * (total_out / 256 + 1024))));
     HIPCHK(sh->nls.alloc((size_t)nl_need + 64));
     if (!sh->ev[0])
         for (auto &e : sh->ev) HIPCHK(hipEventCreate(&e));
@@ -589,8 +590,12 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
                                   sh->info.p + b0, sh->base.p + b0, sh->total.p, nb, sh->nls.p));
     HIPCHK(hipMemcpyAsync(sh->h_tot, sh->total.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipEventRecord(sh->ev[2], s));
+    // descriptors at the batch's shard-global record base (sh->total_records: batches of one shard
+    // run one after the other), writes bounded by the buffer
+    const uint64_t r0 = 4 * (uint64_t)sh->total_records;
     HIPCHK(ppg_launch_parse_emit(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
-                                 sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p, (uint64_t)sh->recs.n, nb));
+                                 sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p + std::min<uint64_t>(r0, sh->recs.n),
+                                 sh->recs.n > r0 ? (uint64_t)sh->recs.n - r0 : 0, nb));
     HIPCHK(hipEventRecord(sh->ev[3], s));
     return PPG_OK;
 }
@@ -606,17 +611,31 @@ int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms) {
     HIPCHK(hipEventElapsedTime(&a, sh->ev[0], sh->ev[1]));
     HIPCHK(hipEventElapsedTime(&b, sh->ev[1], sh->ev[2]));   // counts + scan
     HIPCHK(hipEventElapsedTime(&c, sh->ev[2], sh->ev[3]));   // descriptors
-    if ((size_t)(4 * tot) > sh->recs.n) {
-        HIPCHK(sh->recs.alloc((size_t)(4 * tot + 4096)));
+    const uint64_t r0 = 4 * (uint64_t)sh->total_records;
+    if ((size_t)(r0 + 4 * tot) > sh->recs.n) {
+        // grow, keeping the earlier batches' descriptors, and write this batch's again
+        DevBuf<uint32_t> grown;
+        HIPCHK(grown.alloc((size_t)(r0 + 4 * tot + (r0 + 4 * tot) / 8 + 4096)));
+        if (r0) HIPCHK(hipMemcpyAsync(grown.p, sh->recs.p, 4 * r0, hipMemcpyDeviceToDevice, s));
+        std::swap(grown.p, sh->recs.p);
+        std::swap(grown.n, sh->recs.n);
         HIPCHK(hipEventRecord(sh->ev[2], s));
         HIPCHK(ppg_launch_parse_emit(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
-                                     sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p, (uint64_t)sh->recs.n,
-                                     nb));
+                                     sh->info.p + b0, sh->base.p + b0, sh->nls.p, sh->recs.p + r0,
+                                     (uint64_t)sh->recs.n - r0, nb));
         HIPCHK(hipEventRecord(sh->ev[3], s));
         HIPCHK(hipEventSynchronize(sh->ev[3]));
         float c2 = 0;
         HIPCHK(hipEventElapsedTime(&c2, sh->ev[2], sh->ev[3]));
         c += c2;
+    }
+    // spot keys of the batch's records while its output is resident (ppg_shard_set_keys); the next
+    // batch's inflate follows on the same stream, so this output is read before it is overwritten
+    if (sh->keys_dev) {
+        if (sh->total_records + (int64_t)tot > sh->keys_cap) return PPG_BUF_ERROR;
+        HIPCHK(ppg_launch_record_keys(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
+                                      sh->info.p + b0, sh->base.p + b0, sh->recs.p + r0,
+                                      sh->keys_dev + sh->total_records, nb));
     }
     sh->t_inflate += a;
     sh->t_parse += b + c;
@@ -650,8 +669,7 @@ int shard_finish(ppg_shard *sh, float total_ms) {
 
 extern "C" {
 
-int ppg_shard_run(ppg_shard *sh) {
-    if (!sh) return PPG_ARG_ERROR;
+static int shard_run(ppg_shard *sh) {
     HIPCHK(hipSetDevice(sh->ctx->device));
     shard_reset(sh);
     float total_ms = 0;
@@ -661,6 +679,12 @@ int ppg_shard_run(ppg_shard *sh) {
         if (rc != PPG_OK) return rc;
     }
     return shard_finish(sh, total_ms);
+}
+
+int ppg_shard_run(ppg_shard *sh) {
+    if (!sh) return PPG_ARG_ERROR;
+    sh->last_rc = shard_run(sh);
+    return sh->last_rc;
 }
 
 // Side points: deflate block starts strictly inside the shard's chunks (absolute file bit,
@@ -799,13 +823,20 @@ int ppg_shard_copy_chunk(ppg_shard *sh, int32_t k, uint8_t *dst, int64_t cap, in
 }
 
 int ppg_shard_copy_records(ppg_shard *sh, int32_t k, uint32_t *dst, int64_t cap, int64_t *nrec) {
-    if (!sh || !sh->ran || sh->batches.size() != 1 || k < 0 || k >= sh->n) return PPG_ARG_ERROR;
+    if (!sh || !sh->ran || k < 0 || k >= sh->n) return PPG_ARG_ERROR;
     HIPCHK(hipSetDevice(sh->ctx->device));
     const int64_t r = (int64_t)sh->h_info[(size_t)k].records;
     if (nrec) *nrec = r;
     if (!dst) return PPG_OK;
     if (r > cap) return PPG_BUF_ERROR;
     if (r) HIPCHK(hipMemcpy(dst, sh->recs.p + 4 * sh->h_base[(size_t)k], 16 * (size_t)r, hipMemcpyDeviceToHost));
+    return PPG_OK;
+}
+
+int ppg_shard_set_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap) {
+    if (!sh || cap < 0 || (dev_keys == nullptr) != (cap == 0)) return PPG_ARG_ERROR;
+    sh->keys_dev = dev_keys;
+    sh->keys_cap = cap;
     return PPG_OK;
 }
 

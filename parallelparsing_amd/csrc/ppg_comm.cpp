@@ -20,6 +20,7 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <atomic>
 #include <chrono>
@@ -68,12 +69,21 @@ Rccl &rccl() {
         }                                                                                           \
     } while (0)
 
-// shared-memory all-gather between the processes of one machine (sense-reversing barrier)
+// shared-memory all-gather between the processes of one machine (sense-reversing barrier).  Rank 0
+// creates the segment (O_EXCL: a name must be unique per job, a stale segment is never reused),
+// zeroes it and publishes magic + nranks last; the other ranks join only after seeing both.  A
+// barrier that times out poisons the segment: every later call on it fails instead of miscounting.
 struct ShmHdr {
     std::atomic<uint64_t> arrive;
     std::atomic<uint64_t> gen;
+    std::atomic<uint64_t> magic;
+    std::atomic<uint64_t> nranks;
+    std::atomic<uint64_t> poison;
 };
+static_assert(sizeof(ShmHdr) <= 64, "header fits the segment's first 64 bytes");
+constexpr uint64_t kShmMagic = 0x7070677368636F6Dull;   // "ppgshcom"
 constexpr int64_t kShmSlot = 8 << 20;   // bytes per rank per all-gather (1M chunk counts)
+constexpr int kShmTimeoutS = 300;
 
 }  // namespace
 
@@ -82,15 +92,22 @@ struct ppg_comm {
     int device = -1;                    // RCCL: the GPU the communicator was made for
     ncclComm_t nccl = nullptr;
     bool own_nccl = false;
+    // RCCL: the gathers run on the communicator's own stream, from buffers it owns; the status
+    // phase's buffer is allocated when the comm is made, so nothing can fail before a rank joins it
+    hipStream_t stream = nullptr;
+    DevBuf<int64_t> stat;               // [0] = this rank's (status, width), [2..] = every rank's
+    DevBuf<int64_t> data;               // the padded counts (grown between the two phases)
     // host transport
     std::string shm_name;
     ShmHdr *hdr = nullptr;
     uint8_t *slots = nullptr;
     size_t map_len = 0;
+    bool poisoned = false;
 
     bool host() const { return hdr != nullptr; }
 
     int barrier() {
+        if (poisoned || hdr->poison.load(std::memory_order_acquire)) return PPG_IO_ERROR;
         const uint64_t g = hdr->gen.load(std::memory_order_acquire);
         if (hdr->arrive.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint64_t)nranks) {
             hdr->arrive.store(0, std::memory_order_relaxed);
@@ -100,7 +117,13 @@ struct ppg_comm {
         const auto t0 = std::chrono::steady_clock::now();
         while (hdr->gen.load(std::memory_order_acquire) == g) {
             std::this_thread::yield();
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(300)) return PPG_IO_ERROR;
+            if (hdr->poison.load(std::memory_order_acquire)) { poisoned = true; return PPG_IO_ERROR; }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(kShmTimeoutS)) {
+                // the arrive count is now wrong for every later barrier: the comm is dead
+                poisoned = true;
+                hdr->poison.store(1, std::memory_order_release);
+                return PPG_IO_ERROR;
+            }
         }
         return PPG_OK;
     }
@@ -113,6 +136,26 @@ struct ppg_comm {
         for (int32_t r = 0; r < nranks; r++) memcpy((uint8_t *)recv + (size_t)r * bytes, slots + (size_t)r * kShmSlot,
                                                     (size_t)bytes);
         return barrier();   // nobody overwrites a slot before every rank has read it
+    }
+
+    // RCCL all-gather of n int64 per rank: send = buf[0, n), recv = buf[n, n + n * nranks), on
+    // the comm's stream; host copies in and out.  A failed copy in still enters the collective
+    // (with stale data: the others are waiting) and is reported through sent_ok; an error return
+    // means the collective itself failed.
+    int rccl_all_gather(DevBuf<int64_t> &buf, const int64_t *send, int64_t *recv, size_t n, bool &sent_ok) {
+        sent_ok = hipMemcpyAsync(buf.p, send, 8 * n, hipMemcpyHostToDevice, stream) == hipSuccess;
+        RCCLCHK(rccl().all_gather(buf.p, buf.p + n, n, ncclInt64, nccl, stream));
+        HIPCHK(hipMemcpyAsync(recv, buf.p + n, 8 * n * (size_t)nranks, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        return PPG_OK;
+    }
+
+    // RCCL side state, made with the communicator (on its device)
+    int rccl_setup() {
+        HIPCHK(hipSetDevice(device));
+        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHK(stat.alloc(2 * ((size_t)nranks + 1)));
+        return PPG_OK;
     }
 };
 
@@ -139,6 +182,7 @@ int ppg_comm_init(ppg_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *id,
     memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
     RCCLCHK(rccl().init_rank(&c->nccl, nranks, u, rank));
     c->own_nccl = true;
+    if (int rc = c->rccl_setup()) { ppg_comm_free(c.release()); return rc; }
     *out = c.release();
     return PPG_OK;
 }
@@ -151,6 +195,7 @@ int ppg_comm_from_rccl(ppg_ctx *ctx, void *nccl_comm, int32_t nranks, int32_t ra
     c->rank = rank;
     c->device = ctx->device;
     c->nccl = (ncclComm_t)nccl_comm;
+    if (int rc = c->rccl_setup()) { ppg_comm_free(c.release()); return rc; }
     *out = c.release();
     return PPG_OK;
 }
@@ -162,25 +207,65 @@ int ppg_comm_init_host(int32_t nranks, int32_t rank, const char *name, ppg_comm 
     c->rank = rank;
     c->shm_name = name;
     c->map_len = 64 + (size_t)nranks * kShmSlot;
-    const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
-    if (fd < 0) return PPG_IO_ERROR;
-    if (ftruncate(fd, (off_t)c->map_len) != 0) { close(fd); return PPG_IO_ERROR; }
-    void *p = mmap(nullptr, c->map_len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (p == MAP_FAILED) return PPG_IO_ERROR;
-    c->hdr = (ShmHdr *)p;
+    const auto t0 = std::chrono::steady_clock::now();
+    void *p = MAP_FAILED;
+    if (rank == 0) {
+        // a fresh segment (zero-filled by ftruncate); an existing name is an error, never reused
+        const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0) return PPG_IO_ERROR;
+        if (ftruncate(fd, (off_t)c->map_len) == 0)
+            p = mmap(nullptr, c->map_len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) { shm_unlink(name); return PPG_IO_ERROR; }
+        c->hdr = (ShmHdr *)p;
+        c->hdr->nranks.store((uint64_t)nranks, std::memory_order_relaxed);
+        c->hdr->magic.store(kShmMagic, std::memory_order_release);   // published last
+    } else {
+        // wait for rank 0's segment: it exists, has its full size and carries magic + nranks
+        for (;;) {
+            const int fd = shm_open(name, O_RDWR, 0600);
+            if (fd >= 0) {
+                struct stat st;
+                if (fstat(fd, &st) == 0 && (size_t)st.st_size >= c->map_len)
+                    p = mmap(nullptr, c->map_len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+                close(fd);
+                if (p != MAP_FAILED) {
+                    ShmHdr *h = (ShmHdr *)p;
+                    if (h->magic.load(std::memory_order_acquire) == kShmMagic) {
+                        if (h->nranks.load(std::memory_order_relaxed) != (uint64_t)nranks) {
+                            munmap(p, c->map_len);
+                            return PPG_ARG_ERROR;
+                        }
+                        break;
+                    }
+                    munmap(p, c->map_len);
+                    p = MAP_FAILED;
+                }
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(kShmTimeoutS)) return PPG_IO_ERROR;
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        c->hdr = (ShmHdr *)p;
+    }
     c->slots = (uint8_t *)p + 64;
-    // every rank has mapped the segment (zero-filled by ftruncate) before any gather starts
-    if (int rc = c->barrier()) { munmap(p, c->map_len); return rc; }
+    // every rank has mapped the segment before any gather starts
+    if (int rc = c->barrier()) {
+        munmap(p, c->map_len);
+        if (rank == 0) shm_unlink(name);
+        return rc;
+    }
     *out = c.release();
     return PPG_OK;
 }
 
 void ppg_comm_free(ppg_comm *c) {
     if (!c) return;
-    if (c->nccl && c->own_nccl) {
+    if (c->nccl) {
         if (c->device >= 0) (void)hipSetDevice(c->device);
-        (void)rccl().destroy(c->nccl);
+        if (c->own_nccl) (void)rccl().destroy(c->nccl);
+        c->stat.release();
+        c->data.release();
+        if (c->stream) (void)hipStreamDestroy(c->stream);
     }
     if (c->hdr) {
         munmap((void *)c->hdr, c->map_len);
@@ -225,36 +310,58 @@ int ppg_partition(const ppg_index *ix, int32_t first, int32_t n, int32_t nranks,
 
 }  // extern "C"
 
-// The count all-gather: every rank contributes `local` (its chunks' record counts) and its status;
-// a rank that failed still takes part (the others would wait for it forever), and every rank
-// returns the first failing rank's status.  ctx may be NULL for a host-transport comm.
+// The count all-gather, in two phases that every rank always enters, failed or not (a rank that
+// returned early would leave the others waiting in the collective forever):
+//   1. (status, width) of every rank, from a buffer allocated with the comm -- a failing rank,
+//      one whose bounds are bad or whose data buffer cannot be allocated says so here;
+//   2. only if every rank is fine (each rank decides from the same gathered statuses): the
+//      per-chunk counts padded to the widest range (RCCL has no all-gatherv).
+// Every rank returns the first failing rank's status.  bounds may be NULL (a rank that could not
+// partition); ctx may be NULL (a host-transport comm, or a failed rank).
 static int gather_counts(ppg_comm *comm, ppg_ctx *ctx, const std::vector<int64_t> &local, int status,
                          const int32_t *bounds, int64_t *counts, int64_t *bases, int64_t *total_records) {
     const int32_t R = comm->nranks;
     int32_t width = 1;
-    for (int32_t r = 0; r < R; r++) {
-        if (bounds[r + 1] < bounds[r]) return PPG_ARG_ERROR;
-        width = std::max(width, bounds[r + 1] - bounds[r]);
+    if (!bounds) {
+        if (status == PPG_OK) status = PPG_ARG_ERROR;
+    } else {
+        for (int32_t r = 0; r < R; r++) {
+            if (bounds[r + 1] < bounds[r]) { if (status == PPG_OK) status = PPG_ARG_ERROR; width = 1; break; }
+            width = std::max(width, bounds[r + 1] - bounds[r]);
+        }
+        if (status == PPG_OK && (int64_t)local.size() != bounds[comm->rank + 1] - bounds[comm->rank])
+            status = PPG_ARG_ERROR;
     }
-    const int32_t W = width + 1;                       // + the rank's status
+    const int32_t W = width;
+    const bool rccl_path = !comm->host();
+    if (rccl_path) {
+        if (hipSetDevice(comm->device) != hipSuccess && status == PPG_OK) status = PPG_DEVICE_ERROR;
+        if (ctx && comm->device != ctx->device && status == PPG_OK) status = PPG_ARG_ERROR;
+        if (status == PPG_OK && comm->data.alloc((size_t)W * (R + 1)) != hipSuccess) status = PPG_MEM_ERROR;
+    } else if (8 * (int64_t)W > kShmSlot && status == PPG_OK) {
+        status = PPG_UNSUPPORTED;
+    }
+    // phase 1: statuses and widths
+    int64_t mine[2] = {status, W};
+    std::vector<int64_t> all(2 * (size_t)R, 0);
+    bool sent_ok = true;
+    // a failed collective (RCCL error, host-transport timeout / poison) is the only early return
+    if (int rc1 = rccl_path ? comm->rccl_all_gather(comm->stat, mine, all.data(), 2, sent_ok)
+                            : comm->host_all_gather(mine, all.data(), 16))
+        return rc1;
+    for (int32_t r = 0; r < R; r++)
+        if (all[2 * (size_t)r] != 0) return (int)all[2 * (size_t)r];
+    for (int32_t r = 0; r < R; r++)
+        if (all[2 * (size_t)r + 1] != W) return PPG_ARG_ERROR;   // ranks disagree on the bounds
+    if (!sent_ok) status = PPG_DEVICE_ERROR;   // the others saw a stale "ok": gather anyway, then fail
+    // phase 2: the counts
     std::vector<int64_t> send((size_t)W, 0), recv((size_t)W * R, 0);
     std::copy(local.begin(), local.end(), send.begin());
-    send[(size_t)width] = status;
-    if (comm->host()) {
-        if (int rc = comm->host_all_gather(send.data(), recv.data(), 8 * (int64_t)W)) return rc;
-    } else {
-        if (!ctx || comm->device != ctx->device) return PPG_ARG_ERROR;
-        HIPCHK(hipSetDevice(ctx->device));
-        hipStream_t s = ctx->stream;
-        DevBuf<int64_t> d;
-        HIPCHK(d.alloc((size_t)W * (R + 1)));
-        HIPCHK(hipMemcpyAsync(d.p, send.data(), 8 * (size_t)W, hipMemcpyHostToDevice, s));
-        RCCLCHK(rccl().all_gather(d.p, d.p + W, (size_t)W, ncclInt64, comm->nccl, s));
-        HIPCHK(hipMemcpyAsync(recv.data(), d.p + W, 8 * (size_t)W * R, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-    }
-    for (int32_t r = 0; r < R; r++)
-        if (recv[(size_t)r * W + width] != 0) return (int)recv[(size_t)r * W + width];
+    const int rc2 = rccl_path ? comm->rccl_all_gather(comm->data, send.data(), recv.data(), (size_t)W, sent_ok)
+                              : comm->host_all_gather(send.data(), recv.data(), 8 * (int64_t)W);
+    if (status != PPG_OK) return status;
+    if (rc2 != PPG_OK) return rc2;
+    if (!sent_ok) return PPG_DEVICE_ERROR;
     int64_t run = 0;
     size_t o = 0;
     for (int32_t r = 0; r < R; r++)
@@ -275,16 +382,21 @@ extern "C" {
 // counts / bases (may be NULL) receive bounds[nranks] - bounds[0] entries in canonical order.
 int ppg_shard_gather_counts(ppg_shard *sh, ppg_comm *comm, const int32_t *bounds, int64_t *counts, int64_t *bases,
                             int64_t *total_records) {
-    if (!sh || !comm || !bounds) return PPG_ARG_ERROR;
+    if (!comm) return PPG_ARG_ERROR;   // nothing to join
+    // from here on every path joins the gather: the other ranks wait for this one
     int status = PPG_OK;
     std::vector<int64_t> local;
-    if (!sh->ran || bounds[comm->rank + 1] - bounds[comm->rank] != sh->n) {
-        status = PPG_ARG_ERROR;                        // still take part: the other ranks wait
+    if (!sh) {
+        status = PPG_ARG_ERROR;
+    } else if (sh->last_rc != PPG_OK) {
+        status = sh->last_rc;                          // the rank's own DecompressAll failed
+    } else if (!sh->ran || !bounds || bounds[comm->rank + 1] - bounds[comm->rank] != sh->n) {
+        status = PPG_ARG_ERROR;
     } else {
         local.resize((size_t)sh->n);
         for (int32_t i = 0; i < sh->n; i++) local[(size_t)i] = (int64_t)sh->h_info[(size_t)i].records;
     }
-    const int rc = gather_counts(comm, sh->ctx, local, status, bounds, counts, bases, total_records);
+    const int rc = gather_counts(comm, sh ? sh->ctx : nullptr, local, status, bounds, counts, bases, total_records);
     return status != PPG_OK ? status : rc;
 }
 
@@ -294,28 +406,33 @@ int ppg_shard_gather_counts(ppg_shard *sh, ppg_comm *comm, const int32_t *bounds
 // bases (may be NULL) get one entry per chunk of the index in canonical order.
 int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, const char *gz_path,
                             int64_t out_capacity, int64_t *counts, int64_t *bases, int64_t *total_records) {
-    if (!ctx || !comm || !ix || !gz_path || ix->pts.size() < 1) return PPG_ARG_ERROR;
-    const int32_t n = (int32_t)ix->pts.size() - 1;
-    std::vector<int32_t> bounds((size_t)comm->nranks + 1);
-    if (int rc = ppg_partition(ix, 0, n, comm->nranks, bounds.data())) return rc;
-    const int32_t a = bounds[(size_t)comm->rank], b = bounds[(size_t)comm->rank + 1];
-    const int fd = open(gz_path, O_RDONLY);
-    struct FdClose { int fd; ~FdClose() { if (fd >= 0) close(fd); } } fdc{fd};
-    const int64_t lo = ix->pts[(size_t)a].input - 1, len = ix->pts[(size_t)b].input - ix->pts[(size_t)a].input + 1;
-    PinnedBuf pin;
-    int rc = fd < 0 ? PPG_IO_ERROR
+    if (!comm) return PPG_ARG_ERROR;   // nothing to join
+    // from here on every path joins the gather: a failure is everyone's result, never a hang
+    int rc = (!ctx || !ix || !gz_path || ix->pts.size() < 1) ? PPG_ARG_ERROR : PPG_OK;
+    std::vector<int32_t> bounds((size_t)comm->nranks + 1, 0);
+    if (rc == PPG_OK) rc = ppg_partition(ix, 0, (int32_t)ix->pts.size() - 1, comm->nranks, bounds.data());
+    std::vector<int64_t> local;
+    if (rc == PPG_OK) {
+        const int32_t a = bounds[(size_t)comm->rank], b = bounds[(size_t)comm->rank + 1];
+        const int fd = open(gz_path, O_RDONLY);
+        struct FdClose { int fd; ~FdClose() { if (fd >= 0) close(fd); } } fdc{fd};
+        const int64_t lo = ix->pts[(size_t)a].input - 1, len = ix->pts[(size_t)b].input - ix->pts[(size_t)a].input + 1;
+        PinnedBuf pin;
+        rc = fd < 0 ? PPG_IO_ERROR
              : hipSetDevice(ctx->device) == hipSuccess && pin.alloc((size_t)std::max<int64_t>(len, 1)) == hipSuccess
                  ? PPG_OK : PPG_DEVICE_ERROR;
-    if (rc == PPG_OK && len > 0 && !pread_parallel(fd, pin.p, lo, len, 8)) rc = PPG_IO_ERROR;
-    ppg_shard *sh = nullptr;
-    if (rc == PPG_OK) rc = ppg_shard_create(ctx, ix, a, b - a, pin.p, len, 0, out_capacity, &sh);
-    if (rc == PPG_OK) rc = ppg_shard_run(sh);
-    std::vector<int64_t> local((size_t)(b - a), 0);
-    if (rc == PPG_OK)
-        for (int32_t i = 0; i < b - a; i++) local[(size_t)i] = (int64_t)sh->h_info[(size_t)i].records;
-    ppg_shard_free(sh);
-    // every rank gathers, failed or not: a failure is everyone's result, never a hang
-    const int grc = gather_counts(comm, ctx, local, rc, bounds.data(), counts, bases, total_records);
+        if (rc == PPG_OK && len > 0 && !pread_parallel(fd, pin.p, lo, len, 8)) rc = PPG_IO_ERROR;
+        ppg_shard *sh = nullptr;
+        if (rc == PPG_OK) rc = ppg_shard_create(ctx, ix, a, b - a, pin.p, len, 0, out_capacity, &sh);
+        if (rc == PPG_OK) rc = ppg_shard_run(sh);
+        if (rc == PPG_OK) {
+            local.resize((size_t)(b - a));
+            for (int32_t i = 0; i < b - a; i++) local[(size_t)i] = (int64_t)sh->h_info[(size_t)i].records;
+        }
+        ppg_shard_free(sh);
+    }
+    const int grc = gather_counts(comm, ctx, local, rc, rc == PPG_OK ? bounds.data() : nullptr, counts, bases,
+                                  total_records);
     return rc != PPG_OK ? rc : grc;
 }
 

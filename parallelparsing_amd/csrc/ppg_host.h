@@ -156,7 +156,7 @@ struct ppg_shard {
     DevBuf<uint64_t> base;     // record base within the batch
     DevBuf<uint64_t> total;
     DevBuf<uint8_t> out;
-    DevBuf<uint32_t> recs;
+    DevBuf<uint32_t> recs;     // descriptors of every record of the run, shard-global (all batches)
     DevBuf<uint32_t> nls;      // newline census of the inflate flush (PpgInflateJob::nl_off/nl_cap)
     int64_t out_cap = 0;
     std::vector<std::pair<int32_t, int32_t>> batches;   // chunk ranges [b0, b1) relative to first
@@ -171,6 +171,10 @@ struct ppg_shard {
     hipStream_t stream = nullptr;   // null: the ctx stream (ppg_file_decompress_all gives each piece shard its own)
     uint64_t *h_tot = nullptr;      // pinned: a batch's record total, read back without a stream sync
     int ran = 0;
+    int last_rc = PPG_OK;           // status of the last ppg_shard_run (the count gather forwards it)
+    // ppg_shard_set_keys: every batch also writes its records' spot keys here (global record number)
+    int64_t *keys_dev = nullptr;
+    int64_t keys_cap = 0;
     // split chunks (ppg_shard_set_split): the inflate launch runs sub-jobs, ppg_split_merge folds
     // them back into per-chunk results and census regions
     int32_t nsub = 0;                            // side points in use (0: one wave per chunk)

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 
@@ -88,6 +89,16 @@ struct __attribute__((aligned(16))) InflateLds {
     uint8_t lens[320];
     uint32_t cen[8];               // newline census: count, previous byte was '\n', PPG_PF_* flags, cap, shift, dst
 };
+
+#ifdef PPG_STAMPS
+// diagnostic build only (EXTRA=-DPPG_STAMPS): s_memtime stamps at the phase boundaries of every
+// token round, summed per wave and added to these totals at the end of each chunk; the launcher
+// prints them (cycles per phase, rounds) after each launch.  Perturbs the schedule (+~10%).
+__device__ unsigned long long ppg_stamp_acc[8];
+#define PPG_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#else
+#define PPG_STAMP(t)
+#endif
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
@@ -309,7 +320,9 @@ __device__ __forceinline__ void flush_census(const uint8_t *ring, uint8_t *out, 
             nact = min(left / 16, 64u);
             if ((uint32_t)lane < nact) {
                 const uint4 v = *(const uint4 *)(ring + ((uint32_t)(g + 16 * lane) & RM));
+#ifndef PPG_PROBE_NO_STORE   // timing probe only (A/B): no output stores, far bytes read garbage
                 *(uint4 *)(out + g + 16 * lane) = v;
+#endif
                 w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
             }
             lastbit = 15;
@@ -352,9 +365,15 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, con
 // No wait states precede the load: the base pair must not be written by a VALU (a spill restore)
 // just before it -- tools/hazard_lint.py checks the compiled kernel for that at every build (with
 // amdgpu_num_sgpr(64) the base was spilled and the load faulted; padding costs 0.6%).
+// PPG_FAR_NOP pads the load with the 5 wait states (builds whose SGPR pressure spills the base).
+#ifdef PPG_FAR_NOP
+#define PPG_FAR_PAD "s_nop 4\n\t"
+#else
+#define PPG_FAR_PAD ""
+#endif
 __device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) {
     uint32_t v;
-    asm volatile("global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+    asm volatile(PPG_FAR_PAD "global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
     return v;
 }
 
@@ -550,6 +569,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         }
     };
     uint32_t nblk = 0;
+#ifdef PPG_STAMPS
+    uint64_t sa_dec = 0, sa_walk = 0, sa_rd = 0, sa_far = 0, sa_dep = 0, sa_tail = 0, sa_rounds = 0, sa_farr = 0;
+#endif
 #ifdef PPG_STATS
     // debug build only (EXTRA=-DPPG_STATS): per-chunk round / token / path counts, printed for the
     // first chunks (tools/ab_bench.sh-style runs; DESIGN.md quotes them)
@@ -689,6 +711,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         // the next round's decode over this round's far loads measured no gain: at 8 waves per
         // SIMD the kernel is issue-bound, chiefly on SALU — see DESIGN.md.)
         uint32_t bp = rd_pos(r);
+#ifdef PPG_STAMPS
+        uint64_t st_w0 = 0;        // stamp: the round's spec tokens are decoded, the walk starts
+#endif
         uint32_t cn = 0, cw = 0;   // carried: bytes left of the last round's last match, its token word
 
         // decode of the round starting at output position pos, stream bit bp, carry (cn, cw):
@@ -727,6 +752,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 // Per token: 2 VALU, 3 SALU, 1 branch.
                 constexpr uint32_t STOP = 0x1C0C0u;   // s >= 64 (bits 7:6) or off >= 64 (bits 16:14)
                 uint32_t X;
+#ifdef PPG_STAMPS
+                st_w0 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(vta ^ vtb);
+#endif
                 if (len - pos >= 64) {
                     X = off << 8;
 #ifdef PPG_WALK_PRIO
@@ -800,8 +828,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 
         for (;;) {
             // ---- one round: decode + walk, then one output byte per lane ----
+            PPG_STAMP(t0);
             st_enter(r, S.stream, bp >> 10, lane);
             const Round R = decode(bp, cn, cw, pos);
+#ifdef PPG_STAMPS
+            const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
+            if (st_w0 < t0) st_w0 = t1;   // no walk this round
+            sa_dec += st_w0 - t0;
+            sa_walk += t1 - st_w0;
+            sa_rounds++;
+#endif
 #ifdef PPG_STATS
             st_rounds++;
             st_tokens += (uint32_t)__popcll(__ballot(R.vtin != 0));
@@ -838,6 +874,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #ifdef PPG_STATS
                 if (fm) st_far++;
 #endif
+#ifdef PPG_STAMPS
+                const uint64_t t2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
+                sa_rd += t2 - t1;
+#endif
 #ifdef PPG_PROBE_NO_FAR
                 if (false) {   // timing probe only: far bytes read from the ring (wrong output)
 #else
@@ -865,6 +905,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                         val = fd ? db : val;
                     }
                 }
+#ifdef PPG_STAMPS
+                const uint64_t t3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
+                sa_far += t3 - t2;
+                sa_farr += fm ? 1 : 0;
+#endif
                 const bool dep = jj >= 0;                             // produced in this round
                 if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
@@ -897,6 +942,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 }
 #endif
                 S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
+#ifdef PPG_STAMPS
+                const uint64_t t4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
+                sa_dep += t4 - t3;
+                st_w0 = t4;   // reused below: start of the round's tail
+#endif
 #if (defined(PPG_DEC_PRIO) || defined(PPG_EMIT_PRIO)) && !defined(PPG_TAIL_PRIO)
                 asm volatile("s_setprio 0");
 #endif
@@ -921,6 +971,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             if constexpr (IX) {   // past the member, or runaway output (a false start)
                 if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
             }
+#ifdef PPG_STAMPS
+            sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
+            st_w0 = 0;
+#endif
             if (!R.spec) {
                 if (pos < len) continue;
                 break;
@@ -992,6 +1046,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                "bitserial lit %u eob %u match %u\n", k, pos, st_rounds, st_tokens, st_spec, st_short, st_far, st_dep,
                st_dbl, st_blit, st_beob, st_bmatch);
 #endif
+#ifdef PPG_STAMPS
+    if (!IX && lane == 0) {
+        atomicAdd(&ppg_stamp_acc[0], (unsigned long long)sa_dec);
+        atomicAdd(&ppg_stamp_acc[1], (unsigned long long)sa_walk);
+        atomicAdd(&ppg_stamp_acc[2], (unsigned long long)sa_rd);
+        atomicAdd(&ppg_stamp_acc[3], (unsigned long long)sa_far);
+        atomicAdd(&ppg_stamp_acc[4], (unsigned long long)sa_dep);
+        atomicAdd(&ppg_stamp_acc[5], (unsigned long long)sa_tail);
+        atomicAdd(&ppg_stamp_acc[6], (unsigned long long)sa_rounds);
+        atomicAdd(&ppg_stamp_acc[7], (unsigned long long)sa_farr);
+    }
+#endif
     if (lane == 0) {
         res[k].produced = pos;
         res[k].end_bit = w0abs * 32 + end_bit;
@@ -1009,6 +1075,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 // ------------------------------------------------------------------------------------------
 // (ring bits, litlen root bits) variants; default (11, 9)
 #define PPG_VARIANTS(X) X(10, 8) X(10, 9) X(11, 9) X(11, 8) X(12, 9) X(12, 8) X(13, 9) X(15, 9)
+
+#ifdef PPG_STAMPS
+struct PpgStampPrinter;
+static void ppg_stamp_dump(hipStream_t s);
+#define PPG_STAMP_DUMP(s) ppg_stamp_dump(s)
+#else
+#define PPG_STAMP_DUMP(s)
+#endif
 
 size_t ppg_inflate_lds_bytes(int ring_bits, int lit_bits) {
 #define X(R, L) if (ring_bits == R && lit_bits == L) return sizeof(InflateLds<R, L>);
@@ -1033,12 +1107,30 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
         else                                                                                                  \
             hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, false>), dim3(njobs), dim3(64),               \
                                sizeof(InflateLds<R, L>), s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls); \
+        PPG_STAMP_DUMP(s);                                                                                    \
         return hipGetLastError();                                                                             \
     }
     PPG_VARIANTS(X)
 #undef X
     return hipErrorInvalidValue;
 }
+
+#ifdef PPG_STAMPS
+// diagnostic build: print and reset the per-phase round totals (after the stream drains)
+struct PpgStampPrinter {
+    static void dump(hipStream_t s) {
+        unsigned long long h[8] = {0};
+        if (hipStreamSynchronize(s) != hipSuccess) return;
+        if (hipMemcpyFromSymbol(h, HIP_SYMBOL(ppg_stamp_acc), sizeof h) != hipSuccess) return;
+        const unsigned long long z[8] = {0};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(ppg_stamp_acc), z, sizeof z);
+        const double r = h[6] ? (double)h[6] : 1.0;
+        fprintf(stderr, "PPG_STAMPS rounds %llu far-rounds %llu cycles/round: decode %.1f walk %.1f read %.1f far %.1f "
+                        "dep+write %.1f tail %.1f total %.1f\n", h[6], h[7], h[0] / r, h[1] / r, h[2] / r, h[3] / r,
+                h[4] / r, h[5] / r, (h[0] + h[1] + h[2] + h[3] + h[4] + h[5]) / r);
+    }
+};
+#endif
 
 // CreateIndex pass 1: jobs decode whole blocks into 64 KiB output rings (out + k * 64 KiB)
 hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
@@ -1049,3 +1141,7 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
                        nwords, jobs, dicts, out, res, njobs, blk, nullptr);
     return hipGetLastError();
 }
+
+#ifdef PPG_STAMPS
+static void ppg_stamp_dump(hipStream_t s) { PpgStampPrinter::dump(s); }
+#endif

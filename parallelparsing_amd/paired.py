@@ -22,11 +22,28 @@ DUP = -2      # key of a record parsed twice (Q1), dropped before pairing
 NOKEY = -1    # identifier without an "SRR<id>.<spot>." field
 
 
+def attach_keys(shard, max_records):
+    """Give a shard a device key buffer that every output batch of its later runs fills
+    (ppg_shard_set_keys): pairing then works on shards of any number of batches, e.g. configs[4]'s
+    2 x 25 GB on one GPU, whose outputs cannot both stay resident."""
+    import torch
+    keys = torch.empty(max(1, int(max_records)), dtype=torch.int64, device=torch.device("cuda", shard.dev.device))
+    shard.dev.wait_stream(torch.cuda.current_stream(keys.device))   # the block may be recycled
+    return shard.set_keys(keys)
+
+
 def shard_keys(shard):
-    """Spot numbers of all records of a one-batch shard, in record order, as a device tensor
-    (int64; DUP / NOKEY markers kept).  GPU kernel ppg_record_keys."""
+    """Spot numbers of all records of a shard, in record order, as a device tensor (int64; DUP /
+    NOKEY markers kept).  GPU kernel ppg_record_keys: run per batch during the shard's run when
+    attach_keys() gave it a buffer, else (one-batch shards) extracted now."""
     import torch
     n = shard.total_records
+    if getattr(shard, "_keys", None) is not None:
+        if n > shard._keys.numel():
+            raise ValueError("key buffer smaller than the shard's records")
+        # the keys were written on the ctx stream: torch's stream must not read them earlier
+        shard.dev.stream_wait(torch.cuda.current_stream(shard._keys.device))
+        return shard._keys[:n]
     dev = torch.device("cuda", shard.dev.device)
     keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     # the kernel writes on the ctx's stream: torch's caching allocator may have handed out a block

@@ -68,6 +68,39 @@ class TiledFile:
         self.p_offlen, self._p_at = ol[:npts].copy(), at[:npts].copy()
         self.npoints = int(npts)
 
+    # ---- sharing one build between the ranks of a job (bench.py, N > 1) ----
+    _ARRAYS = ("text", "seg", "header", "tail", "block_bit_end", "block_out_end", "p_output", "p_input", "p_bits",
+               "p_offlen", "_p_at")
+    _SCALARS = ("records", "repeats", "chunksize", "blank_lines", "seg_crc", "file_len", "npoints")
+
+    def save(self, d):
+        """Write the member's description (segment text, deflated segment, block list, points) to
+        directory d, e.g. under /dev/shm, for TiledFile.load; "ready" is written last."""
+        import json
+        import os
+        os.makedirs(d, exist_ok=True)
+        for k in self._ARRAYS:
+            np.save(os.path.join(d, k.lstrip("_") + ".npy"), getattr(self, k))
+        with open(os.path.join(d, "meta.json"), "w") as f:
+            json.dump({k: (bool(v) if isinstance(v, (bool, np.bool_)) else int(v))
+                       for k in self._SCALARS for v in [getattr(self, k)]}, f)
+        with open(os.path.join(d, "ready"), "w") as f:
+            f.write("ok")
+
+    @classmethod
+    def load(cls, d):
+        """The TiledFile saved in d, its arrays memory-mapped read-only (no rebuild, no copy: the
+        ranks of one node share the pages)."""
+        import json
+        import os
+        t = cls.__new__(cls)
+        with open(os.path.join(d, "meta.json")) as f:
+            for k, v in json.load(f).items():
+                setattr(t, k, v)
+        for k in cls._ARRAYS:
+            setattr(t, k, np.load(os.path.join(d, k.lstrip("_") + ".npy"), mmap_mode="r"))
+        return t
+
     def expected_records(self):
         """Records DecompressAll emits for the whole member: every record once, plus one duplicate
         per Point that falls exactly on a record start (its offset then holds the whole previous

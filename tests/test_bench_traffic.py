@@ -1,0 +1,43 @@
+"""roofline.traffic is quoted from profiles/traffic.json only for the build it measured
+(VERDICT r02 weak #6): the file names the workload and the library build (ppg_version +
+ppg_build_id, a hash of the inflate object); any other build gets null."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import parallelparsing_amd as pp  # noqa: E402
+
+W = "configs[2]: ~50 GB .fastq.gz per GPU, chunk=10000"
+
+
+def _write(tmp_path, **kw):
+    t = {"workload": W, "hbm_bytes_per_launch": 1.5e12, "build": pp.build_info()}
+    t.update(kw)
+    p = tmp_path / "traffic.json"
+    p.write_text(json.dumps(t))
+    return str(p)
+
+
+def test_build_id_names_the_inflate_object():
+    b = pp.build_info()
+    assert b["build_id"].startswith("inflate-") and len(b["build_id"]) == len("inflate-") + 16
+    assert "gfx950" in b["ppg_version"]
+
+
+def test_matching_build_is_quoted(tmp_path):
+    assert bench.pmc_traffic(W, pp.build_info(), _write(tmp_path)) == 1.5e12
+
+
+def test_stale_build_is_refused(tmp_path):
+    stale = dict(pp.build_info(), build_id="inflate-0123456789abcdef")
+    assert bench.pmc_traffic(W, pp.build_info(), _write(tmp_path, build=stale)) is None
+    # a file from before builds were recorded
+    assert bench.pmc_traffic(W, pp.build_info(), _write(tmp_path, build=None)) is None
+
+
+def test_other_workload_is_refused(tmp_path):
+    assert bench.pmc_traffic("configs[1]: 1 M-read .fastq.gz, chunk=10000", pp.build_info(), _write(tmp_path)) is None

@@ -98,3 +98,79 @@ def test_host_comm_rendezvous_world3():
     for p in procs:
         p.join(60)
     assert got == [(0, 3), (1, 3), (2, 3)]
+
+
+def _failing_rank(rank, world, name, path, chunksize, bad, q):
+    """ppg_dist_decompress_all through the C ABI with no device context (this container has no
+    GPU): every rank fails before decoding, one also with no index; all must still meet in the
+    gather and return the same status instead of leaving the others waiting."""
+    import ctypes as C
+    import os as _os
+    import parallelparsing_amd as pp
+    from parallelparsing_amd._lib import lib
+    try:
+        ix = pp.Core.BuildDeflateIndex(path, chunksize)
+        comm = pp.Comm.host(world, rank, name)
+        m = ix.Count - 1
+        counts, bases = (C.c_int64 * m)(), (C.c_int64 * m)()
+        tot = C.c_int64(-1)
+        rc = lib.ppg_dist_decompress_all(None, comm.handle, None if (bad and rank == 1) else ix.handle,
+                                         _os.fsencode(path), 0, counts, bases, C.byref(tot))
+        # the comm is still usable afterwards: a second call meets again and fails again
+        rc2 = lib.ppg_dist_decompress_all(None, comm.handle, ix.handle, _os.fsencode(path), 0, counts, bases,
+                                          C.byref(tot))
+        comm.close()
+        q.put((rank, rc, rc2))
+    except Exception as e:   # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e), None))
+
+
+@pytest.mark.parametrize("bad", [False, True])
+def test_failing_ranks_all_return_the_same_status(bad, tmp_path):
+    """a rank that fails never returns before the collective."""
+    import uuid
+    import torch.multiprocessing as mp
+    from parallelparsing_amd._lib import PPG_ARG_ERROR
+    meta, gz = load_case("l6_c200")
+    p = tmp_path / "f.gz"
+    p.write_bytes(gz)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/ppg_cpu_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_failing_rank, args=(r, 2, name, str(p), meta["chunksize"], bad, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = sorted(q.get(timeout=120) for _ in procs)
+    for pr in procs:
+        pr.join(60)
+    assert got == [(0, PPG_ARG_ERROR, PPG_ARG_ERROR), (1, PPG_ARG_ERROR, PPG_ARG_ERROR)], got
+
+
+def _stale_name_rank(name, q):
+    import parallelparsing_amd as pp
+    try:
+        pp.Comm.host(2, 0, name)
+        q.put("opened")
+    except pp.PpgError as e:
+        q.put(e.code)
+
+
+def test_host_comm_refuses_a_stale_segment():
+    """rank 0 never reuses an existing segment of the same name (stale arrive /
+    generation counters would release the first barrier early)."""
+    import uuid
+    import torch.multiprocessing as mp
+    from parallelparsing_amd._lib import PPG_IO_ERROR
+    name = f"/ppg_cpu_{uuid.uuid4().hex[:12]}"
+    path = "/dev/shm" + name
+    with open(path, "wb") as f:   # what a crashed job leaves behind
+        f.write(b"\1" * 4096)
+    try:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        pr = ctx.Process(target=_stale_name_rank, args=(name, q))
+        pr.start()
+        assert q.get(timeout=60) == PPG_IO_ERROR
+        pr.join(30)
+    finally:
+        os.remove(path)

@@ -48,3 +48,36 @@ def test_bench_paired_two_ranks_same_pairs():
     two = _bench(args, ranks=2)
     assert one["config"]["pairs"] == two["config"]["pairs"] == 300000
     assert two["n_gpus"] == 2 and two["config"]["pair_check"].startswith("all_to_all")
+
+
+def test_bench_rccl_glue_world1():
+    """The bench's N > 1 glue under nccl = RCCL, at world size 1 (one GPU on this box): the process
+    group, rank 0's ppg_comm_unique_id broadcast, ppg_comm_init, and ppg_shard_gather_counts over
+    RCCL every step (VERDICT r02 next #2)."""
+    env = dict(os.environ, PPG_BENCH_FORCE_DIST="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PPG_BENCH_ONE_DEVICE", "PPG_DIST_BACKEND"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(29000 + os.getpid() % 400),
+           os.path.join(ROOT, "bench.py")] + SMALL
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    c = line["communicator"]
+    assert c["backend"] == "nccl" and c["world_size"] == 1
+    assert c["count_gather"] == "libppgpu ppg_shard_gather_counts over RCCL (ncclAllGather)"
+    one = _bench(SMALL)
+    assert line["config"]["records"] == one["config"]["records"]
+    assert len(line["setup_s"]["per_rank"]) == 1
+
+
+def test_bench_shares_the_input_between_ranks():
+    """N > 1: local rank 0 builds the member once and the other ranks memory-map it from /dev/shm
+    (VERDICT r02 next #2); the shared copy is gone after the run."""
+    import glob
+    before = set(glob.glob("/dev/shm/ppg_bench_*"))
+    two = _bench(SMALL + ["--gpus", "2"])
+    st = two["setup_s"]
+    assert st["input_how"].startswith("built (shared via /dev/shm/")
+    assert len(st["per_rank"]) == 2
+    assert set(glob.glob("/dev/shm/ppg_bench_*")) == before

@@ -148,3 +148,69 @@ def test_abi_gather_multi_rank_on_one_gpu(world, tmp_path, device):
         assert c1 == exp and c2 == exp and b1 == exp_b and b2 == exp_b
         assert t1 == t2 == meta["total_records"]
         assert bounds[0] == 0 and bounds[-1] == len(exp) and len(bounds) == world + 1
+
+
+def _rank_bad(rank, world, name, path, chunksize, q):
+    try:
+        import parallelparsing_amd as pp2
+        dev = pp2.Device(0)
+        ix = pp2.Core.BuildDeflateIndex(path, chunksize)
+        comm = pp2.Comm.host(world, rank, name)
+        codes = []
+        # rank 1 names a file that does not exist: every rank must get its IO_ERROR, none may hang
+        try:
+            pp2.dist_decompress_all(ix, path if rank == 0 else path + ".missing", comm, device=dev)
+            codes.append(0)
+        except pp2.PpgError as e:
+            codes.append(e.code)
+        # then a shard whose run failed (rank 0: a corrupt compressed range) joins the count gather
+        bounds = pp2.partition(ix, world)
+        a, b = int(bounds[rank]), int(bounds[rank + 1])
+        _, i0, _, _ = ix.point_fields(a)
+        _, i1, _, _ = ix.point_fields(b)
+        with open(path, "rb") as f:
+            f.seek(i0 - 1)
+            comp = np.frombuffer(f.read(i1 - i0 + 1), np.uint8).copy()
+        if rank == 0:
+            comp[len(comp) // 3:] ^= 0x5A
+        sh = pp2.Shard(ix, comp, a, b - a, device=dev)
+        try:
+            sh.run()
+        except pp2.PpgError:
+            pass
+        try:
+            pp2.gather_counts(sh, comm, bounds)
+            codes.append(0)
+        except pp2.PpgError as e:
+            codes.append(e.code)
+        # and the comm still works for a good round afterwards
+        sh2 = pp2.Shard(ix, np.frombuffer(open(path, "rb").read()[i0 - 1:i1], np.uint8), a, b - a, device=dev).run()
+        _, _, tot = pp2.gather_counts(sh2, comm, bounds)
+        comm.close()
+        q.put((rank, codes, tot))
+    except Exception as e:   # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e), None))
+
+
+def test_failing_rank_never_leaves_the_others_waiting(tmp_path, device):
+    """a rank whose input is unreadable, or whose DecompressAll failed, still
+    joins the count gather; every rank returns the first failing rank's status."""
+    import torch.multiprocessing as mp
+    from parallelparsing_amd._lib import PPG_IO_ERROR
+    meta, gz = load_case("l6_c200")
+    p = tmp_path / "f.gz"
+    p.write_bytes(gz)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/ppg_test_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_rank_bad, args=(r, 2, name, str(p), meta["chunksize"], q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for pr in procs:
+        pr.join(60)
+    assert all(r[2] == meta["total_records"] for r in res), res
+    c0, c1 = res[0][1], res[1][1]
+    assert c0 == c1, res
+    assert c0[0] == PPG_IO_ERROR
+    assert c0[1] < 0     # rank 0's own decode error, returned by both ranks

@@ -2,7 +2,9 @@
 reference's LibZ, Interop/PlatformInterop.cs:6-35).  No .NET SDK exists in this image, so the
 sources cannot be compiled here; this checks them against include/ppgpu.h instead: PpGpu.cs
 declares exactly the header's entry points, each with the header's parameter count, and the
-enumerator only calls externs PpGpu.cs declares."""
+enumerator only calls externs PpGpu.cs declares, and every parameter and return type maps to its
+C# marshalling type (int64_t <-> long, uint32_t <-> uint, T* <-> T* / out T / nint, char* <->
+string, ...), so a drift in either file fails here (VERDICT r02 weak #8)."""
 import os
 import re
 
@@ -59,3 +61,84 @@ def test_batch_struct_layout_matches_header():
     cs_fields = re.findall(r"public [\w\*]+ (\w+);", sb)
     norm = lambda x: x.replace("_", "").lower()   # noqa: E731
     assert [norm(f) for f in c_fields] == [norm(f) for f in cs_fields]
+
+
+# ---- type-level check: include/ppgpu.h parameter / return types -> allowed C# types ----
+_SCALAR = {"int": "int", "int32_t": "int", "int64_t": "long", "uint32_t": "uint", "float": "float",
+           "double": "double"}
+_OPAQUE = {"ppg_ctx", "ppg_index", "ppg_shard", "ppg_cursor", "ppg_comm"}
+
+
+def _c_params():
+    """name -> (return type, [param types]) with const and parameter names stripped."""
+    src = re.sub(r"/\*.*?\*/", "", _read("include", "ppgpu.h"), flags=re.S)
+    out = {}
+    for m in re.finditer(r"([\w\s\*]+?)\b(ppg_\w+)\s*\(([^;{]*?)\)\s*;", src):
+        ret = re.sub(r"\bconst\b", "", m.group(1)).split("\n")[-1].strip()
+        args = m.group(3).strip()
+        params = []
+        if args not in ("", "void"):
+            for a in args.split(","):
+                a = re.sub(r"\bconst\b", "", a).strip()
+                t = re.match(r"^([\w\s]+?)\s*(\**)\s*\w+$", a)
+                assert t, (m.group(2), a)
+                params.append(t.group(1).strip() + t.group(2))
+        out[m.group(2)] = (re.sub(r"\s+", "", ret), params)
+    return out
+
+
+def _cs_params():
+    src = _read("interop", "PpGpu.cs")
+    out = {}
+    for m in re.finditer(r"extern\s+([\w\*]+)\s+(ppg_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.S):
+        args = re.sub(r"/\*.*?\*/", "", m.group(3)).strip()
+        params = []
+        if args:
+            for a in args.split(","):
+                toks = a.split()
+                params.append(" ".join(toks[:-1]))   # drop the parameter name
+        out[m.group(2)] = (m.group(1), params)
+    return out
+
+
+def _allowed(ctype, ret=False):
+    """C# spellings that marshal the C type `ctype` (no const, no names)."""
+    base, stars = ctype.rstrip("*"), len(ctype) - len(ctype.rstrip("*"))
+    if stars == 0:
+        if base == "void":
+            return {"void"}
+        return {_SCALAR[base]}
+    if base in _OPAQUE:
+        return {"nint"} if stars == 1 else {"out nint"}
+    if stars == 1 and base == "char":
+        return {"nint"} if ret else {"string"}
+    if stars == 1 and base == "ppg_batch":
+        return {"out PpgBatch", "PpgBatch*"}
+    if stars == 1 and base == "void":
+        return {"nint"} if ret else {"void*", "nint", "byte*"}
+    if stars == 1 and base == "uint8_t":
+        return {"byte*"}
+    if stars == 1 and base in _SCALAR:
+        cs = _SCALAR[base]
+        return {cs + "*", "out " + cs}
+    raise AssertionError(f"no C# mapping for C type {ctype!r}")
+
+
+def test_pinvoke_types_match_header():
+    c, cs = _c_params(), _cs_params()
+    assert sorted(c) == sorted(cs)
+    for name, (ret, params) in c.items():
+        cret, cparams = cs[name]
+        assert cret in _allowed(ret, ret=True), (name, "return", ret, cret)
+        assert len(cparams) == len(params), name
+        for i, (ct, cst) in enumerate(zip(params, cparams)):
+            assert cst in _allowed(ct), (name, i, ct, cst)
+
+
+def test_type_check_catches_drift():
+    """The mapping is strict: a long where the header has uint32_t, or a plain pointer for an
+    opaque out-handle, is rejected."""
+    assert "long" not in _allowed("uint32_t")
+    assert "int" not in _allowed("int64_t")
+    assert "nint" not in _allowed("ppg_index**")
+    assert "byte*" not in _allowed("int64_t*")

@@ -50,6 +50,8 @@ def main(tag):
     n = nf[inf]
     out = {
         "workload": b["config"]["workload"],
+        # the library the counters were taken on (bench.py refuses the file for any other build)
+        "build": b.get("build"),
         "command": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE, separate pass) -- "
                    "python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest",
         "kernel": short(inf),
