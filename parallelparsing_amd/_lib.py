@@ -152,6 +152,10 @@ def synth():
         s.ppg_synth_fastq_size_mate.argtypes = [i64, i64, C.c_int, C.c_int]
         s.ppg_synth_fastq_mate.restype = i64
         s.ppg_synth_fastq_mate.argtypes = [C.c_uint64, C.c_int, i64, i64, C.c_int, vp, i64, C.c_int]
+        s.ppg_synth_illumina_size.restype = i64
+        s.ppg_synth_illumina_size.argtypes = [C.c_uint64, i64, i64]
+        s.ppg_synth_illumina.restype = i64
+        s.ppg_synth_illumina.argtypes = [C.c_uint64, i64, i64, vp, i64, C.c_int]
         s.ppg_synth_gzip.restype = i64
         s.ppg_synth_gzip.argtypes = [vp, i64, C.c_int, i64, C.c_int, vp, i64]
         s.ppg_synth_segment.restype = i64

@@ -97,9 +97,98 @@ int64_t write_rec(char *p, uint64_t seed, int64_t no, int L, int mate = 0) {
     return p - p0;
 }
 
+// ---- "Illumina-like" records: what real SRA FASTQ looks like, unlike the
+// Generator shape -- variable read lengths (70% 151 bp, else 35..151), N bases, and Phred+33
+// qualities over '!'..'J' that include '@' (Q31): about 1.2% of quality bytes, so CreateIndex's
+// '@' count (Core.cs:86-94) sees "records" inside quality lines and Points land mid-record
+// (SURVEY Q2).  Header "@SRR6750041.{no+1} {no+1} length={L}", '+' line the same with '+'.
+inline int ill_len(uint64_t seed, int64_t no) {
+    uint64_t s = seed * 0xA0761D6478BD642Full ^ ((uint64_t)no * 0xE7037ED1A0B428DBull) ^ 0x8EBC6AF09C88C6E3ull;
+    const uint64_t r = splitmix(s);
+    return (r & 1023) < 717 ? 151 : 35 + (int)((r >> 10) % 117);
+}
+
+inline int64_t ill_hdr(int64_t no, int L) {   // "SRR6750041." + no+1 + " " + no+1 + " length=" + L + "\n"
+    return 11 + 2 * digits((uint64_t)no + 1) + 1 + 8 + digits((uint64_t)L) + 1;
+}
+
+inline int64_t ill_size(uint64_t seed, int64_t no) {
+    const int L = ill_len(seed, no);
+    return 2 * (1 + ill_hdr(no, L)) + 2 * (int64_t)(L + 1);
+}
+
+int64_t write_ill(char *p, uint64_t seed, int64_t no) {
+    const int L = ill_len(seed, no);
+    uint64_t s = seed * 0x9FB21C651E98DF25ull ^ ((uint64_t)no * 0xC2B2AE3D27D4EB4Full) ^ 0x165667B19E3779F9ull;
+    splitmix(s);
+    char *p0 = p;
+    char *seq = nullptr;
+    for (int line = 0; line < 2; line++) {
+        *p++ = line == 0 ? '@' : '+';
+        memcpy(p, "SRR6750041.", 11); p += 11;
+        p += put_u(p, (uint64_t)no + 1);
+        *p++ = ' ';
+        p += put_u(p, (uint64_t)no + 1);
+        memcpy(p, " length=", 8); p += 8;
+        p += put_u(p, (uint64_t)L);
+        *p++ = '\n';
+        if (line == 0) {
+            seq = p;
+            for (int i = 0; i < L; i++) {
+                const uint64_t r = splitmix(s);
+                p[i] = (r & 1023) < 4 ? 'N' : "ACGT"[(r >> 10) & 3];
+            }
+            p += L;
+            *p++ = '\n';
+        }
+    }
+    for (int i = 0; i < L; i++) {
+        const uint64_t r = splitmix(s);
+        const uint32_t u = (uint32_t)(r & 0xFFFF), v = (uint32_t)(r >> 16);
+        char q;
+        if (seq[i] == 'N') q = (v & 1) ? '!' : '#';
+        else if (u < 1311) q = '#';                                   // 2%: Q2, Illumina's low-quality tail
+        else if (u < 3277) q = (char)('!' + v % 11);                   // 3%: Q0..Q10
+        else if (u < 19661) q = (char)(',' + v % 21);                  // 25%: Q11..Q31 (',' .. '@')
+        else q = (char)('A' + v % 10);                                 // Q32..Q41 ('A' .. 'J')
+        p[i] = q;
+    }
+    p += L;
+    *p++ = '\n';
+    return p - p0;
+}
+
 }  // namespace
 
 extern "C" {
+
+int64_t ppg_synth_illumina_size(uint64_t seed, int64_t no0, int64_t n) {
+    int64_t t = 0;
+    for (int64_t no = no0; no < no0 + n; no++) t += ill_size(seed, no);
+    return t;
+}
+
+// Illumina-like records [no0, no0+n) into out (cap bytes).  Returns bytes written or -1.
+int64_t ppg_synth_illumina(uint64_t seed, int64_t no0, int64_t n, uint8_t *out, int64_t cap, int threads) {
+    if (threads < 1) threads = 1;
+    const int64_t per = (n + threads - 1) / threads;
+    std::vector<int64_t> off(threads + 1, 0);
+    for (int t = 0; t < threads; t++) {
+        const int64_t a = no0 + std::min(n, t * per), b = no0 + std::min(n, (t + 1) * per);
+        off[t + 1] = off[t] + ppg_synth_illumina_size(seed, a, b - a);
+    }
+    if (off[threads] > cap) return -1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+        th.emplace_back([=, &off] {
+            const int64_t a = no0 + std::min(n, t * per), b = no0 + std::min(n, (t + 1) * per);
+            char *p = (char *)out + off[t];
+            for (int64_t no = a; no < b; no++) p += write_ill(p, seed, no);
+        });
+    }
+    for (auto &x : th) x.join();
+    return off[threads];
+}
 
 // exact byte size of records [no0, no0+n) of file `mate` (0: single file, 1/2: pair mates)
 int64_t ppg_synth_fastq_size_mate(int64_t no0, int64_t n, int read_len, int mate) {
