@@ -67,6 +67,19 @@ def shared_tiled(args, key, build):
     return TiledFile.load(d), time.time() - t, f"memory-mapped from {d}"
 
 
+def gather_pairs(x, y, dist_on, xdev):
+    """[(x, y) of rank 0, (x, y) of rank 1, ...] -- one all_gather (flat output: gloo wants it)."""
+    import torch
+    v = torch.tensor([x, y], dtype=torch.float64, device=xdev)
+    if not dist_on:
+        return [v.tolist()]
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    out = torch.zeros(world * 2, dtype=torch.float64, device=xdev)
+    dist.all_gather_into_tensor(out, v)
+    return out.view(world, 2).cpu().tolist()
+
+
 def drop_shared(args):
     """After every rank has loaded it (a barrier): local rank 0 removes the /dev/shm copy (the
     ranks' mappings stay valid)."""
@@ -187,9 +200,56 @@ def pmc_traffic(workload, build, path=None):
     return t.get("hbm_bytes_per_launch")
 
 
-def ingest_run(tf, ix, dev, threads, piece_gib=8.0):
+def pcie_d2h_GBps(dev, gib=4):
+    """Device -> pinned host copy rate of this box (the bound of any leg that lands decompressed
+    text in host memory): one 4 GiB hipMemcpy, best of three."""
+    import torch
+    n = gib << 30
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    best = 0.0
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        h.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, n / (time.perf_counter() - t) / 1e9)
+    del d, h
+    return best
+
+
+def enumerate_run(tf, ix, path, dev, threads, batch_gib, pcie):
+    """BatchedFASTQ's enumerator through the C ABI (ppg_cursor, BatchedFASTQ.cs:54-98): every
+    record's raw bytes (offset_k ++ chunk_k) and descriptor landed in pinned host memory, batch by
+    batch, from the .gz file in page cache.  PCIe-bound: ~385 B of text per
+    record cross device -> host."""
+    import parallelparsing_amd as pp
+    t0 = time.perf_counter()
+    cur = pp.Cursor(ix, path, batch_bytes=int(batch_gib * (1 << 30)), threads=threads, device=dev)
+    t_open = time.perf_counter() - t0
+    nrec = text = nb = 0
+    t1 = time.perf_counter()
+    for b in cur:
+        nrec += b.nrecords
+        text += int(b.raw_off[-1])
+        nb += 1
+    sec = time.perf_counter() - t1
+    cur.close()
+    assert nrec == tf.expected_records(), (nrec, tf.expected_records())
+    host_bytes = text + 16 * nrec
+    bound = pcie * 1e9 / (host_bytes / nrec)
+    return {"records_per_s": nrec / sec, "records_per_s_incl_open": nrec / (sec + t_open), "seconds": sec,
+            "open_s": t_open, "batches": nb, "batch_GiB": batch_gib, "host_GBps": host_bytes / sec / 1e9,
+            "pcie_d2h_GBps": pcie, "pcie_bound_records_per_s": bound, "frac_of_pcie_bound": nrec / sec / bound,
+            "note": "ppg_cursor: pread -> pinned -> H2D -> decode -> D2H of raw text + descriptors, 3 batches in "
+                    "flight (own stream + worker thread each), buffers sized once at open; records counted, not "
+                    "materialised as objects; not the bench value"}
+
+
+def ingest_run(tf, ix, dev, threads, piece_gib=8.0, enum_gib=0.0):
     """Host-ingest path (ppg_file_decompress_all): the same member written to $TMPDIR as a real
-    file, streamed from page cache through pinned buffers, PCIe and the kernels."""
+    file, streamed from page cache through pinned buffers, PCIe and the kernels.  With enum_gib > 0
+    the enumerator leg (enumerate_run) reads the same file afterwards."""
     import parallelparsing_amd as pp
     path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"ppg_ingest_{os.getpid()}.fastq.gz")
     try:
@@ -202,12 +262,21 @@ def ingest_run(tf, ix, dev, threads, piece_gib=8.0):
         pp.decompress_file(ix, path, device=dev, threads=threads, piece_bytes=pb)   # warm: buffers, page cache
         _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=threads, piece_bytes=pb)
         assert tot == tf.expected_records(), (tot, tf.expected_records())
-        return {"records_per_s": tot / sec, "compressed_GBps": tf.file_len / sec / 1e9,
-                "decompressed_GBps": tf.text_len * tf.repeats / sec / 1e9, "seconds": sec,
-                "file_GB": tf.file_len / 1e9, "write_s": wt,
-                "note": f"file in page cache -> pread ({threads} threads) -> pinned -> H2D -> decode, {piece_gib:g} GiB pieces "
-                        "(three device slots, per-slot streams: a piece's decode overlaps the previous one's tail); "
-                        "PCIe-inclusive, not the bench value"}
+        out = {"records_per_s": tot / sec, "compressed_GBps": tf.file_len / sec / 1e9,
+               "decompressed_GBps": tf.text_len * tf.repeats / sec / 1e9, "seconds": sec,
+               "file_GB": tf.file_len / 1e9, "write_s": wt,
+               "note": f"file in page cache -> pread ({threads} threads) -> pinned -> H2D -> decode, {piece_gib:g} GiB "
+                       "pieces (three device slots, per-slot streams: a piece's decode overlaps the previous one's "
+                       "tail); PCIe-inclusive, not the bench value"}
+        enum = None
+        if enum_gib > 0:
+            try:
+                import torch
+                pcie = pcie_d2h_GBps(torch.device("cuda", dev.device))
+                enum = enumerate_run(tf, ix, path, dev, threads, enum_gib, pcie)
+            except (OSError, AssertionError, RuntimeError) as e:
+                enum = {"error": f"{type(e).__name__}: {e}"}
+        return out, enum
     finally:
         if os.path.exists(path):
             os.remove(path)
@@ -580,6 +649,10 @@ def main():
                     help="skip the end-to-end leg (N = 1): DecompressAll straight from the .gz file on disk (host "
                          "ingest, PCIe-inclusive; reported under 'ingest', never as value)")
     ap.add_argument("--ingest", action="store_true", help=argparse.SUPPRESS)   # on by default since r02
+    ap.add_argument("--no-enumerate", action="store_true",
+                    help="skip the enumerator leg (N = 1, after the ingest leg): every record's bytes and descriptor "
+                         "landed in host memory through ppg_cursor (reported under 'enumerate', never as value)")
+    ap.add_argument("--enum-batch-gib", type=float, default=8.0, help="enumerator leg: text per cursor batch (GiB)")
     args = ap.parse_args()
     if args.seg_records is None:   # the paired files keep 1 GB segments: two members must fit one GPU
         args.seg_records = PAIRED_SEG_RECORDS if args.paired else SEG_RECORDS
@@ -670,14 +743,9 @@ def main():
     comm, gather_via = (None, None) if not dist_on else make_comm(ctx, world, rank, backend, xdev)
     bounds = np.array([r[0] for r in ranges] + [ranges[-1][1]], np.int32)
     # per-rank setup seconds (input ready, shard ready) of every rank, in the line
-    setup = torch.tensor([args.input_seconds, setup_s], dtype=torch.float64, device=xdev)
+    setup_ranks = gather_pairs(args.input_seconds, setup_s, dist_on, xdev)
     if dist_on:
-        allset = torch.zeros(world, 2, dtype=torch.float64, device=xdev)
-        dist.all_gather_into_tensor(allset, setup)
-        setup_ranks = allset.cpu().tolist()
         drop_shared(args)   # every rank has mapped the shared input by now
-    else:
-        setup_ranks = [setup.tolist()]
 
     def step():
         err = None
@@ -808,7 +876,10 @@ def main():
         line["create_index"] = create_index_run(tf, args, dev)
     if rank == 0 and world == 1 and args.ingest:
         try:
-            line["ingest"] = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads, args.ingest_piece_gib)
+            line["ingest"], enum = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads,
+                                              args.ingest_piece_gib, 0 if args.no_enumerate else args.enum_batch_gib)
+            if enum is not None:
+                line["enumerate"] = enum
         except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
             line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -10,6 +10,7 @@
 //  * Count(): ppg_file_decompress_all on one GPU, or ppg_dist_decompress_all when the process is
 //    one rank of a multi-GPU job (GpuJob: the ranks' RCCL communicator).
 // (Source only: no .NET SDK in this image; tests/test_interop_cs.py checks the externs it uses.)
+using System;
 using System.Collections;
 using ParallelParsing.Common;
 using ParallelParsing.Interop;
@@ -79,8 +80,15 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
     private readonly int _Threads;
     private readonly GpuJob? _Job;
 
-    /// <summary>Text per streamed batch; host memory holds about two batches.</summary>
-    public long BatchBytes { get; set; } = 1L << 30;
+    /// <summary>Text per streamed batch (ppg_cursor keeps three batches in flight in pinned host
+    /// memory).  Any size: each chunk is copied into its own managed array (a chunk is below 2^31
+    /// bytes, ppg_index_validate), so a batch may exceed a managed array's limit.</summary>
+    public long BatchBytes
+    {
+        get => _BatchBytes;
+        set => _BatchBytes = value > 0 ? value : throw new ArgumentOutOfRangeException(nameof(value));
+    }
+    private long _BatchBytes = 4L << 30;
 
     /// <summary>Enumerable.Count over the records (Decompressor/Program.cs:48-52), without
     /// materialising them: one GPU streams the file, a multi-GPU job gathers every rank's counts.</summary>
@@ -116,20 +124,21 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
         }
     }
 
-    // The next batch's records, or null after the last batch.  Its raw bytes are copied into one
-    // managed array (the pinned batch is reused by the next ppg_cursor_next) that the records slice.
+    // The next batch's records, or null after the last batch.  Each chunk's raw bytes are copied
+    // into a managed array of their own (the pinned batch is reused by a later ppg_cursor_next) that
+    // its records slice; a chunk's raw_k is below 2^31 bytes (ppg_index_validate), a batch need not be.
     private static unsafe FastqRecord[]? NextBatch(nint cur)
     {
         int rc = PpGpu.ppg_cursor_next(cur, out var b);
         if (rc == (int)ZResult.STREAM_END) return null;
         PpGpu.Check(rc);
-        var text = new byte[b.RawOff[b.NChunks]];
-        new ReadOnlySpan<byte>(b.Text, text.Length).CopyTo(text);
         var recs = new FastqRecord[b.NRecords];
         long o = 0;
         for (int k = 0; k < b.NChunks; k++)
         {
-            var raw = new Memory<byte>(text, (int)b.RawOff[k], (int)(b.RawOff[k + 1] - b.RawOff[k]));
+            var chunk = new byte[b.RawOff[k + 1] - b.RawOff[k]];
+            new ReadOnlySpan<byte>(b.Text + b.RawOff[k], chunk.Length).CopyTo(chunk);
+            var raw = new Memory<byte>(chunk);
             uint start = 0;   // Parsing.cs:19 -- the first record starts at raw[0] ('@' skipped)
             for (long j = b.RecOff[k]; j < b.RecOff[k + 1]; j++)
             {

@@ -6,17 +6,29 @@
 // that surface over the GPU path: the file is cut into batches of whole chunks of at most
 // batch_bytes of text; each batch is read (pread into pinned memory), copied to HBM, decoded
 // (inflate + record scan, the DecompressAll kernels) and brought back as the chunks' raw bytes
-// (offset_k ++ chunk_k, Parsing.cs's CombinedMemory) plus the record descriptors.  Two slots
-// alternate: while the caller walks batch k, batch k+1 is read and decoded on the other slot's
-// stream.  A batch stays valid until the next ppg_cursor_next call (the reference's records are
-// likewise invalid after the next MoveNext, BatchedFASTQ.cs:56 / SURVEY Q9).  Order is canonical
-// (chunk 0's records, then chunk 1's, ...), not the reference's interleaving.
+// (offset_k ++ chunk_k, Parsing.cs's CombinedMemory) plus the record descriptors.
+//
+// What bounds it is PCIe: every byte of text crosses device -> host once (~385 B per record at
+// 150 bp), the compressed input host -> device in the other direction.  So kSlots batches are in
+// flight, each on its own stream and worker thread: while the caller walks batch k, batches k+1
+// and k+2 are being read, decoded and copied back, and the copies of one overlap the decode of
+// the next.  Every slot's buffers -- pinned text / descriptor / compressed staging, device input,
+// output, census -- are sized once at open from the largest batch, so no worker reallocates (a
+// hipHostFree / hipFree can synchronise the device).  An index with side points
+// (ppg_index_build_gpu_side) splits a batch's chunks into several waves when the batch is too
+// small to fill the GPU by itself.
+//
+// A batch stays valid until the next ppg_cursor_next call (the reference's records are likewise
+// invalid after the next MoveNext, BatchedFASTQ.cs:56 / SURVEY Q9).  Order is canonical (chunk 0's
+// records, then chunk 1's, ...), not the reference's interleaving.
 #include "ppg_host.h"
 #include <fcntl.h>
 #include <unistd.h>
 #include <thread>
 
 namespace {
+
+constexpr int kSlots = 3;
 
 struct Slot {
     ppg_shard sh;                       // device state of the batch (its own stream)
@@ -39,8 +51,9 @@ struct ppg_cursor {
     int fd = -1;
     int32_t first = 0, n = 0;
     int threads = 8;
+    bool split = false;                 // batches smaller than ~6 generations of waves split at side points
     std::vector<std::pair<int32_t, int32_t>> batches;
-    Slot slot[2];
+    Slot slot[kSlots];
     size_t next = 0;                    // next batch to hand out
     int64_t record_base = 0;
 
@@ -58,21 +71,51 @@ struct ppg_cursor {
         if (fd >= 0) close(fd);
     }
 
-    // read, decode and bring back batch i into slot s (runs on a worker thread)
+    int64_t comp_len(size_t i) const {
+        const auto &P = ix->pts;
+        return P[(size_t)(first + batches[i].second)].input - P[(size_t)(first + batches[i].first)].input + 1;
+    }
+    int64_t raw_len(size_t i) const {
+        const auto &P = ix->pts;
+        int64_t t = 0;
+        for (int32_t k = first + batches[i].first; k < first + batches[i].second; k++)
+            t += (P[(size_t)k + 1].output - P[(size_t)k].output) + (int64_t)P[(size_t)k].offset.size();
+        return t;
+    }
+
+    // every slot's buffers, once, for the largest batch (the shard's device buffers reach their
+    // size with the first shard_prepare and are then reused: DevBuf::alloc keeps a large enough one)
+    int size_slots() {
+        int64_t cmax = 1, rmax = 1;
+        for (size_t i = 0; i < batches.size(); i++) {
+            cmax = std::max(cmax, comp_len(i));
+            rmax = std::max(rmax, raw_len(i));
+        }
+        for (auto &s : slot) {
+            HIPCHK(s.pcomp.alloc((size_t)cmax));
+            HIPCHK(s.dcomp.alloc((size_t)cmax + 64));
+            HIPCHK(s.text.alloc((size_t)rmax));
+            // descriptors: 16 B per record, for records of >= 64 B on average (grown only beyond)
+            HIPCHK(s.desc.alloc((size_t)(rmax / 4 + 4096)));
+        }
+        return PPG_OK;
+    }
+
+    // read, decode and bring back batch i into slot s (runs on the slot's worker thread)
     int produce(size_t i, Slot &s) {
         if (hipSetDevice(ctx->device) != hipSuccess) return PPG_DEVICE_ERROR;
         const auto &P = ix->pts;
         const int32_t a = first + batches[i].first, b = first + batches[i].second;
         s.b0 = batches[i].first;
         s.b1 = batches[i].second;
-        const int64_t lo = P[(size_t)a].input - 1, len = P[(size_t)b].input - P[(size_t)a].input + 1;
-        HIPCHK(s.pcomp.alloc((size_t)len));
+        const int64_t lo = P[(size_t)a].input - 1, len = comp_len(i);
         if (!pread_parallel(fd, s.pcomp.p, lo, len, threads)) return PPG_IO_ERROR;
         hipStream_t st = s.sh.stream;
-        HIPCHK(s.dcomp.alloc((size_t)len + 64));
         HIPCHK(hipMemsetAsync(s.dcomp.p + len, 0, 64, st));
         HIPCHK(hipMemcpyAsync(s.dcomp.p, s.pcomp.p, (size_t)len, hipMemcpyHostToDevice, st));
         if (int rc = shard_prepare(&s.sh, ix, a, b - a, s.dcomp.p, len, 0, st)) return rc;
+        if (split)
+            if (int rc = shard_split_from_index(&s.sh, ix, a, b - a)) return rc;
         shard_reset(&s.sh);
         float ms = 0;
         if (int rc = batch_launch(&s.sh, 0, s.sh.n)) return rc;
@@ -84,9 +127,10 @@ struct ppg_cursor {
         for (int32_t k = 0; k < m; k++)
             s.raw_off[(size_t)k + 1] = s.raw_off[(size_t)k] + (int64_t)P[(size_t)a + k].offset.size() +
                                        (int64_t)s.sh.h_res[(size_t)k].produced;
-        HIPCHK(s.text.alloc((size_t)std::max<int64_t>(s.raw_off[(size_t)m], 1)));
+        if ((size_t)s.raw_off[(size_t)m] > s.text.n) return PPG_BUF_ERROR;   // produced <= Output span: never
         s.nrec = s.sh.total_records;
-        HIPCHK(s.desc.alloc((size_t)std::max<int64_t>(16 * s.nrec, 16)));
+        if ((size_t)(16 * s.nrec) > s.desc.n) HIPCHK(s.desc.alloc((size_t)(16 * s.nrec + (16 * s.nrec) / 4)));
+        // the chunks' bodies are contiguous on the device; each lands after its offset carry
         for (int32_t k = 0; k < m; k++) {
             const auto &off = P[(size_t)a + k].offset;
             uint8_t *dst = s.text.p + s.raw_off[(size_t)k];
@@ -103,7 +147,7 @@ struct ppg_cursor {
     }
 
     void start(size_t i) {
-        Slot &s = slot[i & 1];
+        Slot &s = slot[i % kSlots];
         s.rc = PPG_OK;
         s.worker = std::thread([this, i, &s] { s.rc = produce(i, s); });
     }
@@ -116,7 +160,7 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
     if (!ctx || !ix || !gz_path || !out || first < 0 || n < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
         return PPG_ARG_ERROR;
     if (int v = ppg_index_validate(ix, first, n)) return v;
-    if (batch_bytes <= 0) batch_bytes = (int64_t)1 << 30;
+    if (batch_bytes <= 0) batch_bytes = (int64_t)4 << 30;
     HIPCHK(hipSetDevice(ctx->device));
     auto c = std::make_unique<ppg_cursor>();
     c->ctx = ctx;
@@ -128,6 +172,7 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
     if (c->fd < 0) return PPG_IO_ERROR;
     // batches: whole chunks, at most batch_bytes of raw text each (at least one chunk)
     const auto &P = ix->pts;
+    int32_t max_chunks = 0;
     for (int32_t a = 0; a < n;) {
         int32_t b = a + 1;
         int64_t raw = (P[(size_t)first + a + 1].output - P[(size_t)first + a].output) + (int64_t)P[(size_t)first + a].offset.size();
@@ -139,13 +184,20 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
             b++;
         }
         c->batches.push_back({a, b});
+        max_chunks = std::max(max_chunks, b - a);
         a = b;
+    }
+    if (!ix->side_out.empty()) {   // the ~6 generations of waves the bench's auto split uses
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        c->split = (int64_t)max_chunks < 6 * 32 * (int64_t)cus;
     }
     for (auto &s : c->slot) {
         s.sh.ctx = ctx;
         HIPCHK(hipStreamCreateWithFlags(&s.sh.stream, hipStreamNonBlocking));
     }
-    if (!c->batches.empty()) c->start(0);
+    if (int rc = c->size_slots()) return rc;
+    for (size_t i = 0; i < c->batches.size() && i < (size_t)kSlots - 1; i++) c->start(i);
     *out = c.release();
     return PPG_OK;
 }
@@ -153,11 +205,15 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
 int ppg_cursor_next(ppg_cursor *c, ppg_batch *b) {
     if (!c || !b) return PPG_ARG_ERROR;
     if (c->next >= c->batches.size()) return PPG_STREAM_END;
-    Slot &s = c->slot[c->next & 1];
+    Slot &s = c->slot[c->next % kSlots];
     if (s.worker.joinable()) s.worker.join();
     if (s.rc != PPG_OK) return s.rc;
-    // the other slot held the batch handed out last time: the caller is done with it
-    if (c->next + 1 < c->batches.size()) c->start(c->next + 1);
+    // the slot of the batch handed out last time is free again: the caller is done with it
+    if (c->next + kSlots - 1 < c->batches.size()) {
+        Slot &f = c->slot[(c->next + kSlots - 1) % kSlots];
+        if (f.worker.joinable()) f.worker.join();
+        c->start(c->next + kSlots - 1);
+    }
     b->first_chunk = c->first + s.b0;
     b->nchunks = s.b1 - s.b0;
     b->record_base = c->record_base;

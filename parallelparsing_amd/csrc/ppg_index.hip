@@ -265,6 +265,22 @@ __device__ __forceinline__ uint32_t sym_entry(uint32_t x, uint32_t y) {
     return x == y ? 0x8000u | x : (((((y - x) & 255u) - 1u) << 8) | x) & 0x7FFFu;   // (mask: corrupt data stays in range)
 }
 
+// entries 4t..4t+3 of piece j's tail: 16-bit symbols straight from pass 1 (tb == nullptr: ta holds
+// 32 Ki u16 per slot, r03), or from two byte tails over two synthetic histories (sym_entry)
+__device__ __forceinline__ void tail4(const uint8_t *ta, const uint8_t *tb, uint32_t slot, uint32_t t, uint32_t e[4]) {
+    if (!tb) {
+        const uint2 v = ((const uint2 *)(ta + (uint64_t)slot * 65536))[t];
+        e[0] = v.x & 0xFFFFu; e[1] = v.x >> 16; e[2] = v.y & 0xFFFFu; e[3] = v.y >> 16;
+#pragma unroll
+        for (int q = 0; q < 4; q++) e[q] &= (e[q] & 0x8000u) ? 0x80FFu : 0x7FFFu;   // corrupt data stays in range
+        return;
+    }
+    const uint32_t xa = ((const uint32_t *)(ta + (uint64_t)slot * 32768))[t];
+    const uint32_t xb = ((const uint32_t *)(tb + (uint64_t)slot * 32768))[t];
+#pragma unroll
+    for (int q = 0; q < 4; q++) e[q] = sym_entry((xa >> (8 * q)) & 255u, (xb >> (8 * q)) & 255u);
+}
+
 __global__ __launch_bounds__(1024) void ppg_resolve_compose_kernel(const uint8_t *__restrict__ ta,
                                                                    const uint8_t *__restrict__ tb,
                                                                    const uint32_t *__restrict__ slots, int np,
@@ -273,19 +289,14 @@ __global__ __launch_bounds__(1024) void ppg_resolve_compose_kernel(const uint8_t
     const int j0 = blockIdx.x * L, j1 = min(np, j0 + L);
     if (j0 >= j1) return;
     for (int j = j0; j < j1; j++) {
-        const uint32_t *a = (const uint32_t *)(ta + (uint64_t)slots[j] * 32768);
-        const uint32_t *b = (const uint32_t *)(tb + (uint64_t)slots[j] * 32768);
         uint32_t nv[16];   // this thread's 32 new entries, two per register
 #pragma unroll
         for (int r = 0; r < 8; r++) {
             const uint32_t t = threadIdx.x + 1024u * r;   // 4 entries 4t..4t+3
-            const uint32_t xa = a[t], xb = b[t];
             uint32_t e[4];
+            tail4(ta, tb, slots[j], t, e);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t v = sym_entry((xa >> (8 * q)) & 255u, (xb >> (8 * q)) & 255u);
-                e[q] = (j == j0 || (v & 0x8000u)) ? v : m[v];
-            }
+            for (int q = 0; q < 4; q++) e[q] = (j == j0 || (e[q] & 0x8000u)) ? e[q] : m[e[q]];
             nv[2 * r] = e[0] | (e[1] << 16);
             nv[2 * r + 1] = e[2] | (e[3] << 16);
         }
@@ -331,16 +342,11 @@ __global__ __launch_bounds__(1024) void ppg_resolve_fill_kernel(const uint8_t *_
     for (int j = j0; j + 1 < j1; j++) {   // W[j1] came from the groups pass
         const uint8_t *src = W + (uint64_t)j * 32768;
         uint32_t *d = (uint32_t *)(W + (uint64_t)(j + 1) * 32768);
-        const uint32_t *a = (const uint32_t *)(ta + (uint64_t)slots[j] * 32768);
-        const uint32_t *b = (const uint32_t *)(tb + (uint64_t)slots[j] * 32768);
         for (uint32_t t = threadIdx.x; t < 8192; t += 1024) {
-            const uint32_t xa = a[t], xb = b[t];
-            uint32_t v = 0;
+            uint32_t e[4], v = 0;
+            tail4(ta, tb, slots[j], t, e);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t e = sym_entry((xa >> (8 * q)) & 255u, (xb >> (8 * q)) & 255u);
-                v |= (e & 0x8000u ? e & 255u : (uint32_t)src[e]) << (8 * q);
-            }
+            for (int q = 0; q < 4; q++) v |= (e[q] & 0x8000u ? e[q] & 255u : (uint32_t)src[e[q]]) << (8 * q);
             d[t] = v;
         }
         __threadfence_block();

@@ -14,10 +14,10 @@
 //                 IX).  Block boundaries do not depend on history bytes, so walking the pieces in
 //                 order proves each start: piece j+1 is real iff the (real) piece j ended exactly
 //                 there; otherwise piece j+1 is redone from where piece j really ended.  The
-//                 history is unknown, so each piece decodes twice with two synthetic histories;
-//                 the two versions of its last 32 KiB (its "tail") tell every byte apart as a
-//                 literal or a copy of history byte i (ppg_resolve_kernel).  FASTQ needs this:
-//                 a header's "length=150" is copied from the previous record's, a chain that runs
+//                 history is unknown, so pass 1's output is symbolic, 16 bits per position: a
+//                 literal byte, or "a copy of history byte i" (r03; r02 decoded every piece twice,
+//                 over two synthetic histories, to tell the two apart).  FASTQ needs this: a
+//                 header's "length=150" is copied from the previous record's, a chain that runs
 //                 back to the piece's start, so tails depend on the starting history.
 //   3. resolve    the exact starting history of every piece, walking the chain of symbolic
 //                 tails from the stream start (one 32 KiB gather per piece).
@@ -144,70 +144,54 @@ struct Builder {
     std::vector<PpgInflateJob> hjobs;
     std::vector<PpgInflateResult> hres;
     std::vector<PpgBlockEnd> hblk;
-    DevBuf<PpgBlockEnd> blk, bigblk;   // block lists: history A at blk_off, B at blk_off + blk_half
-    DevBuf<uint8_t> ring;               // 64 KiB output ring per slot and history
-    DevBuf<uint8_t> pat;                // synthetic histories A (offset 0) and B (offset 32 KiB)
-    DevBuf<uint8_t> ta, tb;             // tails of pass-1 job q at q * 32 KiB, runs A and B
-    std::vector<PpgInflateResult> hres_b;
+    DevBuf<PpgBlockEnd> blk, bigblk;   // block lists of pass-1 job q at blk_off (bigblk: a piece alone)
+    DevBuf<uint8_t> ring;               // 64 Ki 16-bit symbols of output ring per slot
+    DevBuf<uint8_t> ident;              // u16 0..32767: the history symbols, for tails of short pieces
+    DevBuf<uint8_t> ta;                 // symbolic tail (32 Ki u16) of pass-1 job q at q * 64 KiB
     DevBuf<PpgGather> gat;
     DevBuf<uint32_t> diff;
     DevBuf<uint64_t> dpre;
     DevBuf<PpgBlockEnd> dense;
 
     uint32_t nslots = 0;                // pieces + spare slots for speculative redos
-    uint64_t blk_half = 0;              // history B's block lists sit at blk_off + blk_half (never read)
-    DevBuf<PpgInflateJob> jst;          // staged jobs of a pass-1 launch: [A..., B...]
+    DevBuf<PpgInflateJob> jst;          // staged jobs of a pass-1 launch
     DevBuf<PpgInflateResult> rst;
 
-    // pass-1 decode of job slots `which` (ascending), both synthetic histories in one launch
-    // (history A: ring slot q, history B: ring slot nslots + q); refreshes their results, block
-    // lists and both tails
+    // pass-1 decode of job slots `which` (ascending) in one launch, 16-bit symbolic output into
+    // ring slot q; refreshes their results, block lists and symbolic tails
     int run_pass1(const std::vector<uint32_t> &which, bool big) {
         if (which.empty()) return PPG_OK;
         const size_t n = which.size();
-        std::vector<PpgInflateJob> st(2 * n);
+        std::vector<PpgInflateJob> st(n);
         for (size_t i = 0; i < n; i++) {
-            PpgInflateJob a = hjobs[which[i]];
-            a.dict_off = 0;
-            st[i] = a;
-            a.dict_off = kWin;
-            a.out_off = (uint64_t)(nslots + which[i]) * kRing;
-            a.blk_off = big ? a.blk_cap : (uint32_t)(a.blk_off + blk_half);
-            st[n + i] = a;
+            st[i] = hjobs[which[i]];
+            st[i].dict_off = 0;
         }
-        HIPCHK(jst.alloc(2 * n));
-        HIPCHK(rst.alloc(2 * n));
-        HIPCHK(hipMemcpyAsync(jst.p, st.data(), sizeof(PpgInflateJob) * 2 * n, hipMemcpyHostToDevice, s));
-        HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jst.p, pat.p, ring.p, rst.p, big ? bigblk.p : blk.p, (int)(2 * n)));
-        std::vector<PpgInflateResult> r(2 * n);
-        HIPCHK(hipMemcpyAsync(r.data(), rst.p, sizeof(PpgInflateResult) * 2 * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(jst.alloc(n));
+        HIPCHK(rst.alloc(n));
+        HIPCHK(hipMemcpyAsync(jst.p, st.data(), sizeof(PpgInflateJob) * n, hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jst.p, ident.p, ring.p, rst.p, big ? bigblk.p : blk.p, (int)n));
+        std::vector<PpgInflateResult> r(n);
+        HIPCHK(hipMemcpyAsync(r.data(), rst.p, sizeof(PpgInflateResult) * n, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        for (size_t i = 0; i < n; i++) {
-            hres[which[i]] = r[i];
-            hres_b[which[i]] = r[n + i];
-        }
-        // both runs' tails (run A's ring slots, then run B's)
+        for (size_t i = 0; i < n; i++) hres[which[i]] = r[i];
+        // the tails: the last 32 Ki symbols (64 KiB) of each ring, gathered as two 32 KiB byte
+        // halves; a position before the piece's start is history symbol 32768 + p (ident table)
         std::vector<PpgGather> g(2 * n);
         for (size_t i = 0; i < n; i++) {
             const uint32_t q = which[i];
-            g[i] = PpgGather{(uint64_t)q * kRing, 0, hres[q].produced, kRing - 1, 0};
-            g[n + i] = PpgGather{(uint64_t)(nslots + q) * kRing, (uint64_t)kWin, hres_b[q].produced, kRing - 1, 0};
+            const uint64_t endb = 2 * hres[q].produced;   // byte position of the ring's end
+            g[2 * i] = PpgGather{(uint64_t)q * 2 * kRing, (uint64_t)kWin, endb - kWin, 2 * kRing - 1, 0};
+            g[2 * i + 1] = PpgGather{(uint64_t)q * 2 * kRing, (uint64_t)kWin, endb, 2 * kRing - 1, 0};
         }
         HIPCHK(gat.alloc(g.size()));
         HIPCHK(hipMemcpyAsync(gat.p, g.data(), sizeof(PpgGather) * g.size(), hipMemcpyHostToDevice, s));
-        for (size_t i = 0; i < n;) {   // one gather per contiguous run of slots and history
+        for (size_t i = 0; i < n;) {   // one gather per contiguous run of slots
             size_t e = i + 1;
             while (e < n && which[e] == which[e - 1] + 1) e++;
-            HIPCHK(ppg_launch_gather(s, ring.p, pat.p, gat.p + i, ta.p + (uint64_t)which[i] * kWin, nullptr, nullptr,
-                                     (int)(e - i)));
-            HIPCHK(ppg_launch_gather(s, ring.p, pat.p, gat.p + n + i, tb.p + (uint64_t)which[i] * kWin, nullptr,
-                                     nullptr, (int)(e - i)));
+            HIPCHK(ppg_launch_gather(s, ring.p, ident.p, gat.p + 2 * i, ta.p + (uint64_t)which[i] * 2 * kWin, nullptr,
+                                     nullptr, (int)(2 * (e - i))));
             i = e;
-        }
-        for (uint32_t q : which) {   // both runs follow the same bits: same blocks, same sizes
-            const PpgInflateResult &a = hres[q], &b = hres_b[q];
-            if (a.status != b.status || a.produced != b.produced || a.nblocks != b.nblocks || a.end_bit != b.end_bit)
-                return PPG_DEVICE_ERROR;
         }
         if (big) {
             const uint32_t q = which[0];
@@ -311,7 +295,6 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     B.nslots = nslots;
     B.hjobs.resize(nslots);
     B.hres.assign(nslots, PpgInflateResult{});
-    B.hres_b.assign(nslots, PpgInflateResult{});
     B.own_blocks.assign(nslots, {});
     uint64_t nblk_total = 0;
     uint32_t max_cap = 0;
@@ -336,20 +319,15 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     const uint64_t spare_blk = nblk_total;
     nblk_total += (uint64_t)nspare * spare_cap;
     if (nblk_total >= (1ull << 31)) return PPG_UNSUPPORTED;
-    B.blk_half = nblk_total;
     B.hblk.assign(nblk_total, PpgBlockEnd{0, 0});
-    HIPCHK(B.blk.alloc(2 * nblk_total));
-    HIPCHK(B.ring.alloc((size_t)2 * nslots * kRing));
-    HIPCHK(B.ta.alloc((size_t)nslots * kWin));
-    HIPCHK(B.tb.alloc((size_t)nslots * kWin));
+    HIPCHK(B.blk.alloc(nblk_total));
+    HIPCHK(B.ring.alloc((size_t)nslots * 2 * kRing));
+    HIPCHK(B.ta.alloc((size_t)nslots * 2 * kWin));
     {
-        std::vector<uint8_t> pat(2 * kWin);
-        for (int i = 0; i < kWin; i++) {
-            pat[i] = (uint8_t)(i & 255);
-            pat[kWin + i] = (uint8_t)(((i >> 8) + 1 + (i & 255)) & 255);
-        }
-        HIPCHK(B.pat.alloc(pat.size()));
-        HIPCHK(hipMemcpy(B.pat.p, pat.data(), pat.size(), hipMemcpyHostToDevice));
+        std::vector<uint16_t> ident(kWin);
+        for (int i = 0; i < kWin; i++) ident[i] = (uint16_t)i;
+        HIPCHK(B.ident.alloc(2 * kWin));
+        HIPCHK(hipMemcpy(B.ident.p, ident.data(), 2 * kWin, hipMemcpyHostToDevice));
     }
     {
         std::vector<uint32_t> all(m);
@@ -412,7 +390,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
                 const uint64_t span = (J.stop_bit != ~0ull ? J.stop_bit : end_bits) - J.bit_start;
                 J.blk_off = 0;
                 J.blk_cap = (uint32_t)std::min<uint64_t>(span / 10 + 64, 1u << 30);
-                HIPCHK(B.bigblk.alloc(2 * (size_t)J.blk_cap));   // histories A and B
+                HIPCHK(B.bigblk.alloc((size_t)J.blk_cap));
                 int rc = B.run_pass1({q}, true);
                 if (rc) return rc;
                 B.own_blocks[q] = B.hblk_big;
@@ -462,11 +440,11 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         HIPCHK(dsl.alloc(np));
         HIPCHK(maps.alloc((size_t)ppg_resolve_groups((int)np) * kWin));
         HIPCHK(hipMemcpyAsync(dsl.p, sl.data(), 4 * np, hipMemcpyHostToDevice, s));
-        HIPCHK(ppg_launch_resolve(s, B.ta.p, B.tb.p, dsl.p, (int)np, W.p, maps.p));
+        HIPCHK(ppg_launch_resolve(s, B.ta.p, nullptr, dsl.p, (int)np, W.p, maps.p));
         HIPCHK(hipStreamSynchronize(s));
     }
     // pass 1's device state is spent (block lists live on the host): ~190 KiB per slot
-    for (DevBuf<uint8_t> *b : {&B.ring, &B.ta, &B.tb}) b->release();
+    for (DevBuf<uint8_t> *b : {&B.ring, &B.ta, &B.ident}) b->release();
     B.blk.release();
     B.bigblk.release();
     B.dense.release();

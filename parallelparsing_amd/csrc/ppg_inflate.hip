@@ -27,11 +27,16 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <stdio.h>
+#include <type_traits>
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 
-// CreateIndex pass 1 (IX): each job's output lives in a 64 KiB ring of the out buffer (only the
-// last 32 KiB + REACH are ever read back)
+// CreateIndex pass 1 (IX): each job's output lives in a ring of 64 Ki positions of the out buffer
+// (only the last 32 KiB + REACH are ever read back).  Pass 1 does not know a piece's starting
+// history, so its output is SYMBOLIC, 16 bits per position: 0x8000 | byte for a byte the piece's
+// own literals determine, or i (0..32767) for a copy of byte i of the unknown 32 KiB history
+// (position i - 32768) -- one decode gives what two decodes over two synthetic histories gave
+// before r03; ppg_resolve_kernel turns the tails into exact histories.
 #define IX_RING_BYTES 65536u
 #define IX_RING_MASK (IX_RING_BYTES - 1u)
 #define PPG_STR2(x) #x
@@ -72,9 +77,9 @@
 #endif
 #endif
 
-template <int RB, int LBT>
+template <int RB, int LBT, typename RingT = uint8_t>
 struct __attribute__((aligned(16))) InflateLds {
-    uint8_t ring[1u << RB];
+    RingT ring[1u << RB];          // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1)
     uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LBT];
@@ -98,6 +103,15 @@ __device__ unsigned long long ppg_stamp_acc[8];
 #define PPG_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #else
 #define PPG_STAMP(t)
+#endif
+
+// branch-layout hints for the token round (PPG_LIKELY builds): the hot path as fall-through code
+#ifdef PPG_LIKELY
+#define PPG_HOT(c) __builtin_expect(!!(c), 1)
+#define PPG_COLD(c) __builtin_expect(!!(c), 0)
+#else
+#define PPG_HOT(c) (c)
+#define PPG_COLD(c) (c)
 #endif
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
@@ -149,7 +163,7 @@ __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
 // runs up to two words ahead of the decode position and may have entered sg already).
 __device__ __forceinline__ void st_enter(Reader &r, uint32_t *stream, uint32_t g, int lane) {
-    if (g == r.sg || g + 1 == r.sg) return;
+    if (PPG_HOT(g == r.sg || g + 1 == r.sg)) return;
     if (g != r.sg + 1) {
         st_issue(r, stream, g, lane);
         st_issue(r, stream, g + 1, lane);
@@ -208,6 +222,29 @@ __device__ __forceinline__ void flush_range(const uint8_t *ring, uint8_t *out, u
             uint4 v = *(const uint4 *)(ring + (g & RM));
             *(uint4 *)(out + g) = v;
         }
+    }
+}
+
+// flush_range for CreateIndex pass 1's 16-bit symbols: ring positions [glo, ghi) -> out16 (8 per
+// 16-B store)
+template <int RB>
+__device__ __forceinline__ void flush_range_sym(const uint16_t *ring, uint16_t *out, uint64_t glo, uint64_t ghi,
+                                                int lane) {
+    constexpr uint64_t RM = (1ull << RB) - 1;
+    if (ghi <= glo) return;
+    const uint64_t a = (glo + 7) & ~7ull, z = ghi & ~7ull;
+    if (a >= z) {
+        for (uint64_t g0 = glo; g0 < ghi; g0 += 64) {
+            const uint64_t g = g0 + lane;
+            if (g < ghi) out[g] = ring[g & RM];
+        }
+        return;
+    }
+    if (lane < (int)(a - glo)) out[glo + lane] = ring[(glo + lane) & RM];
+    if (lane < (int)(ghi - z)) out[z + lane] = ring[(z + lane) & RM];
+    for (uint64_t g0 = a; g0 < z; g0 += 512) {
+        const uint64_t g = g0 + (uint64_t)lane * 8;
+        if (g < z) *(uint4 *)(out + g) = *(const uint4 *)(ring + (g & RM));
     }
 }
 
@@ -349,12 +386,17 @@ __device__ __forceinline__ void flush_census(const uint8_t *ring, uint8_t *out, 
 // IX (CreateIndex pass 1): the job's output is a 64 KiB ring, position p at ob[p & 0xFFFF].
 template <bool IX = false>
 __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, const uint8_t *dict, int32_t p) {
-    // the two loads differ in width so the compiler cannot fold them into one per-lane base select
-    if (p >= 0) {
-        const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
-        return (*(const uint32_t *)(ob + (q & ~3u)) >> (8 * (q & 3))) & 255u;
+    if constexpr (IX) {   // 16-bit symbols: the job's ring, or the history index itself
+        if (p >= 0) return ((const uint16_t *)ob)[(uint32_t)p & IX_RING_MASK];
+        return 32768u + (uint32_t)p;
+    } else {
+        // the two loads differ in width so the compiler cannot fold them into one per-lane base select
+        if (p >= 0) {
+            const uint32_t q = oa + (uint32_t)p;
+            return (*(const uint32_t *)(ob + (q & ~3u)) >> (8 * (q & 3))) & 255u;
+        }
+        return dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
     }
-    return dict[32768u + (uint32_t)p];   // p >= -32768; only the chunk's first 32 KiB
 }
 
 // One dword per lane from a uniform base + 32-bit lane offset, as global_load_dword's saddr form,
@@ -390,8 +432,8 @@ __device__ __forceinline__ uint32_t far_wait(uint32_t v) {
 }
 
 // One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
-template <int RB, bool IX>
-__device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uint32_t oa, const uint8_t *dict,
+template <int RB, bool IX, typename RingT>
+__device__ __forceinline__ void copy_match(RingT *ring, const uint8_t *ob, uint32_t oa, const uint8_t *dict,
                                            uint32_t rb0, uint32_t pos, uint32_t dist, uint32_t n, int lane) {
     constexpr uint32_t RM = (1u << RB) - 1;
     constexpr uint32_t REACH = (1u << RB) - 64;   // ring bytes a reference may use (see the emit)
@@ -422,7 +464,7 @@ __device__ __forceinline__ void copy_match(uint8_t *ring, const uint8_t *ob, uin
                 uint32_t v;
                 if (back + n <= REACH) v = ring[(dst0 - back) & RM];
                 else v = far_byte<IX>(ob, oa, dict, rel);
-                ring[(dst0 + j) & RM] = (uint8_t)v;
+                ring[(dst0 + j) & RM] = (RingT)v;
             }
         }
     }
@@ -466,6 +508,28 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 template <uint32_t STOPMASK = 0x1C0C0u>
 __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
     uint32_t t, tmp;
+#ifdef PPG_WALK_UNROLL
+    // two tokens per loop trip: the first token's stop test leaves by a not-taken-usually branch,
+    // so a walk of n tokens takes ~n/2 taken branches instead of n
+    asm volatile(
+        "1:\n\t"
+        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], %[M]\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], %[M]\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc0 1b\n"
+        "2:"
+        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
+        : [vt] "v"(vt), [M] "i"(STOPMASK)
+        : "m0", "scc");
+#else
     asm volatile(
         "1:\n\t"
         "v_readlane_b32 %[t], %[vt], %[X]\n\t"
@@ -477,6 +541,7 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
         : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
         : [vt] "v"(vt), [M] "i"(STOPMASK)
         : "m0", "scc");
+#endif
 }
 
 // IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
@@ -505,7 +570,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     constexpr uint32_t UNIT = RB >= 13 ? 4096u : RING / 2;
     static_assert(RB >= 10 && RB <= 15, "ring of 1..32 KiB");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    InflateLds<RB, LBT> &S = *reinterpret_cast<InflateLds<RB, LBT> *>(smem);
+    using RingT = typename std::conditional<IX, uint16_t, uint8_t>::type;   // IX: 16-bit symbols
+    InflateLds<RB, LBT, RingT> &S = *reinterpret_cast<InflateLds<RB, LBT, RingT> *>(smem);
     const int lane = threadIdx.x;
     const int k = blockIdx.x;
     if (k >= njobs) return;
@@ -514,16 +580,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // < 2^31: ppg_index_validate
     const uint32_t rb0 = (uint32_t)out_off;         // ring slot of chunk position p: (rb0 + p) & RM
     const uint8_t *dict = dicts + J.dict_off;       // chunk position p < 0 is dict[32768 + p]
-    const uint8_t *ob = out + (out_off & ~3ull);    // chunk position p >= 0 is ob[oa + p]
-    const uint32_t oa = (uint32_t)(out_off & 3);
+    // chunk position p >= 0 is ob[oa + p] (IX: 16-bit symbol ((uint16_t *)ob)[p & IX_RING_MASK])
+    const uint8_t *ob = IX ? out + 2 * out_off : out + (out_off & ~3ull);
+    const uint32_t oa = IX ? 0u : (uint32_t)(out_off & 3);
 
-    // history: the last RING bytes of the Point's window -> ring slots of positions [-RING, 0)
-    for (uint32_t w0 = 0; w0 < RING / 4; w0 += 64) {
-        const uint32_t w = w0 + lane;
-        const uint32_t v = *(const uint32_t *)(dict + 32768 - RING + 4 * w);
-        const uint32_t slot = rb0 - RING + 4 * w;
+    if constexpr (IX) {
+        // history symbols: position p in [-RING, 0) is history byte 32768 + p
+        for (uint32_t w0 = 0; w0 < RING; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            S.ring[(rb0 - RING + w) & RM] = (uint16_t)(32768u - RING + w);
+        }
+    } else {
+        // history: the last RING bytes of the Point's window -> ring slots of positions [-RING, 0)
+        for (uint32_t w0 = 0; w0 < RING / 4; w0 += 64) {
+            const uint32_t w = w0 + lane;
+            const uint32_t v = *(const uint32_t *)(dict + 32768 - RING + 4 * w);
+            const uint32_t slot = rb0 - RING + 4 * w;
 #pragma unroll
-        for (int q = 0; q < 4; q++) S.ring[(slot + q) & RM] = (uint8_t)(v >> (8 * q));
+            for (int q = 0; q < 4; q++) S.ring[(slot + q) & RM] = (uint8_t)(v >> (8 * q));
+        }
     }
     constexpr bool census = CEN && !IX;
     if (census && lane == 0) {
@@ -559,7 +634,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     auto flush = [&](uint32_t lo, uint32_t hi) {
         if constexpr (IX) {
             const uint64_t g = out_off + (lo & IX_RING_MASK);
-            flush_range<RB>(S.ring, out, g, g + (hi - lo), lane);
+            flush_range_sym<RB>(S.ring, (uint16_t *)out, g, g + (hi - lo), lane);
         } else {
             if constexpr (census) {
                 flush_census<RB>(S.ring, out, out_off, lo, hi, lane, S.cen);
@@ -614,7 +689,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 const uint32_t piece = min(remain - copied, (uint32_t)UNIT);
                 for (uint32_t j0 = 0; j0 < piece; j0 += 64) {
                     const uint32_t j = j0 + lane;
-                    if (j < piece) S.ring[(rb0 + pos + j) & RM] = c8[copied + j];
+                    if (j < piece) S.ring[(rb0 + pos + j) & RM] = (RingT)((IX ? 0x8000u : 0u) | c8[copied + j]);
                 }
                 pos += piece;
                 copied += piece;
@@ -755,7 +830,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #ifdef PPG_STAMPS
                 st_w0 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(vta ^ vtb);
 #endif
-                if (len - pos >= 64) {
+                if (PPG_HOT(len - pos >= 64)) {
                     X = off << 8;
 #ifdef PPG_WALK_PRIO
                     asm volatile("s_setprio " PPG_STR(PPG_WALK_PRIO));
@@ -860,14 +935,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
                 const uint64_t fm = __ballot(far);
                 const int32_t fp = (int32_t)pos + jj;
-                const uint32_t fq = (oa + (uint32_t)fp) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
+                const uint32_t fq = IX ? 2u * ((uint32_t)fp & IX_RING_MASK) : oa + (uint32_t)fp;   // byte offset
                 uint32_t fw = 0;
                 if (fm) fw = far_issue(ob, far && fp >= 0 ? (fq & ~3u) : 0u);
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                uint32_t val;   // (IX: a literal is the symbol 0x8000 | byte; written apart, the DecompressAll
+                                // instance's code is unchanged -- the folded "| 0" moved its schedule)
+                if constexpr (IX) val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
+                else val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
 #else
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                uint32_t val;   // (IX: a literal is the symbol 0x8000 | byte; written apart, the DecompressAll
+                                // instance's code is unchanged -- the folded "| 0" moved its schedule)
+                if constexpr (IX) val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
+                else val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
                 const uint64_t fm = __ballot(far);
 #endif
@@ -881,7 +962,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #ifdef PPG_PROBE_NO_FAR
                 if (false) {   // timing probe only: far bytes read from the ring (wrong output)
 #else
-                if (fm) {
+                if (PPG_HOT(fm)) {
 #endif
                     // older than the ring: the flushed output (this wave's own earlier stores), as
                     // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
@@ -893,15 +974,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     const uint32_t w = far_wait(fw);
 #else
                     const int32_t p = (int32_t)pos + jj;
-                    const uint32_t q = (oa + (uint32_t)p) & (IX ? IX_RING_MASK : 0xFFFFFFFFu);
+                    const uint32_t q = IX ? 2u * ((uint32_t)p & IX_RING_MASK) : oa + (uint32_t)p;   // byte offset
                     const bool fo = far && p >= 0;
                     const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
 #endif
-                    val = fo ? (w >> (8 * (q & 3))) & 255u : val;
+                    val = fo ? (w >> (8 * (q & 3))) & (IX ? 0xFFFFu : 255u) : val;
                     const bool fd = far && p < 0;
                     const uint64_t dm = __ballot(fd);
-                    if (dm) {   // rare: the chunk's first 32 KiB
-                        const uint32_t db = dict[fd ? 32768u + (uint32_t)p : 0u];   // p >= -32768
+                    if (PPG_COLD(dm)) {   // rare: the chunk's first 32 KiB
+                        uint32_t db;
+                        if constexpr (IX) db = 32768u + (uint32_t)p;          // the history symbol itself
+                        else db = dict[fd ? 32768u + (uint32_t)p : 0u];       // p >= -32768
                         val = fd ? db : val;
                     }
                 }
@@ -911,7 +994,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 sa_farr += fm ? 1 : 0;
 #endif
                 const bool dep = jj >= 0;                             // produced in this round
-                if (__ballot(dep)) {
+                if (PPG_COLD(__ballot(dep))) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
                     int32_t ptr = dep ? jj : lane;
 #ifdef PPG_STATS
@@ -941,7 +1024,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     val += (pv ^ (uint32_t)lane) + (ps ^ pos);
                 }
 #endif
-                S.ring[(rb0 + pos + lane) & RM] = (uint8_t)val;
+                S.ring[(rb0 + pos + lane) & RM] = (RingT)val;
 #ifdef PPG_STAMPS
                 const uint64_t t4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
                 sa_dep += t4 - t3;
@@ -956,7 +1039,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
             }
             pos += rout;
-            if (pos >= fl_next) {
+            if (PPG_COLD(pos >= fl_next)) {
 #ifdef PPG_FLUSH_PRIO
                 asm volatile("s_setprio " PPG_STR(PPG_FLUSH_PRIO));
 #endif
@@ -975,8 +1058,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
             st_w0 = 0;
 #endif
-            if (!R.spec) {
-                if (pos < len) continue;
+            if (PPG_HOT(!R.spec)) {
+                if (PPG_HOT(pos < len)) continue;
                 break;
             }
 
@@ -992,7 +1075,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #endif
             if (sym < 0 || sym >= 286) { status = ST_DATA_ERROR; break; }
             if (sym < 256) {
-                if (lane == 0) S.ring[(rb0 + pos) & RM] = (uint8_t)sym;
+                if (lane == 0) S.ring[(rb0 + pos) & RM] = (RingT)((IX ? 0x8000u : 0u) | (uint32_t)sym);
                 pos++;
             } else if (sym == 256) {
                 in_block = 0;
@@ -1005,7 +1088,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
                 const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
                 const uint32_t n = min(ml, len - pos);
-                copy_match<RB, IX>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
+                copy_match<RB, IX, RingT>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
             }
             bp = rd_pos(r);
@@ -1137,7 +1220,8 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs) {
     if (njobs <= 0) return hipSuccess;
-    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64), sizeof(InflateLds<10, 8>), s, comp,
+    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64),
+                       sizeof(InflateLds<10, 8, uint16_t>), s, comp,
                        nwords, jobs, dicts, out, res, njobs, blk, nullptr);
     return hipGetLastError();
 }

@@ -52,3 +52,31 @@ def test_launch_cmd_shape():
     assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
     assert "--nproc-per-node=8" in cmd and "127.0.0.1" in cmd and "--master-port=29511" in cmd
     assert cmd[-3:] == ["--gpus", "8", "--steps", "3"][-3:]
+
+
+def _pairs_rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    q.put((rank, bench.gather_pairs(float(rank), 10.0 + rank, True, "cpu")))
+    dist.destroy_process_group()
+
+
+def test_gather_pairs_gloo_world2():
+    """bench.py's per-rank setup-seconds gather over gloo (the one-GPU rehearsal's backend)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_pairs_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert got[0] == got[1] == [[0.0, 10.0], [1.0, 11.0]]

@@ -113,7 +113,7 @@ def test_realistic_1m_reads_level6_equals_oracle(device):
     gz = gzip_level6(txt)
     ix, sh = _gpu_vs_oracle(gz, txt, 10_000, device)
     q2 = q2_shifted_points(ix, txt)
-    assert ix.Count > 300 and q2 > (ix.Count - 2) // 5, (ix.Count, q2)
+    assert ix.Count > 200 and q2 > (ix.Count - 2) // 5, (ix.Count, q2)
     # the misparse is real: the reference's record count differs from the true one
     assert sh.total_records != 1_000_000
 
