@@ -294,7 +294,7 @@ def create_index_run(tf, args, dev):
     tf.fill_device(gz, 0, tf.file_len)
     torch.cuda.synchronize()
     g = gz[: tf.file_len]
-    runs = []
+    runs, phases = [], []
     ix = None
     for _ in range(2):                                             # first run: allocation warm-up
         ix = None
@@ -302,8 +302,10 @@ def create_index_run(tf, args, dev):
         ix = pp.Core.BuildDeflateIndexGpu(g, args.chunk, out_capacity=int(args.ix_capacity_gib * (1 << 30)),
                                           piece_bytes=int(args.ix_piece_kib * 1024))
         runs.append(time.perf_counter() - t)
-        log(f"[bench] GPU CreateIndex: {runs[-1]:.2f} s, {ix.Count} points")
-    st = pp.Core.gpu_index_stats()
+        st = pp.Core.gpu_index_stats()
+        phases.append({k: round(st[k], 1) for k in ("finder_ms", "pass1_ms", "chain_ms", "resolve_ms", "pass2_ms",
+                                                    "pass2_alloc_ms", "census_ms")})
+        log(f"[bench] GPU CreateIndex: {runs[-1]:.2f} s, {ix.Count} points, phases {phases[-1]}")
     del gz, g
     torch.cuda.empty_cache()
     out, inp, bits = ix.arrays()
@@ -329,7 +331,8 @@ def create_index_run(tf, args, dev):
     csec = time.perf_counter() - t
     assert cix.Count == one.npoints
     cpu_gbs = one.text_len / csec / 1e9
-    return {"seconds": sec, "first_run_s": runs[0], "points": ix.Count, "gz_GBps": tf.file_len / sec / 1e9,
+    return {"seconds": sec, "first_run_s": runs[0], "phases_ms_per_run": phases, "points": ix.Count,
+            "gz_GBps": tf.file_len / sec / 1e9,
             "decompressed_GBps": text / sec / 1e9,
             "phases_ms": {k: round(st[k], 2) for k in ("finder_ms", "pass1_ms", "chain_ms", "resolve_ms", "pass2_ms", "pass2_alloc_ms",
                                                        "census_ms")},

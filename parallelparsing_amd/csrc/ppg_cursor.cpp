@@ -9,12 +9,13 @@
 // (offset_k ++ chunk_k, Parsing.cs's CombinedMemory) plus the record descriptors.
 //
 // What bounds it is PCIe: every byte of text crosses device -> host once (~385 B per record at
-// 150 bp), the compressed input host -> device in the other direction.  So kSlots batches are in
+// 150 bp), the compressed input host -> device in the other direction.  So several batches are in
 // flight, each on its own stream and worker thread: while the caller walks batch k, batches k+1
 // and k+2 are being read, decoded and copied back, and the copies of one overlap the decode of
 // the next.  Every slot's buffers -- pinned text / descriptor / compressed staging, device input,
 // output, census -- are sized once at open from the largest batch, so no worker reallocates (a
-// hipHostFree / hipFree can synchronise the device).  An index with side points
+// hipHostFree / hipFree can synchronise the device).  A batch's raw_k are packed on the device
+// (ppg_pack_raw) and cross PCIe as one copy.  An index with side points
 // (ppg_index_build_gpu_side) splits a batch's chunks into several waves when the batch is too
 // small to fill the GPU by itself.
 //
@@ -24,17 +25,26 @@
 #include "ppg_host.h"
 #include <fcntl.h>
 #include <unistd.h>
+#include <chrono>
 #include <thread>
+
+// launcher (ppg_parse.hip)
+hipError_t ppg_launch_pack_raw(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs, const PpgInflateResult *ires,
+                               const uint8_t *offs, const PpgOffsetRef *oref, const int64_t *raw_off, uint8_t *dst,
+                               int n);
+hipError_t ppg_launch_copy16(hipStream_t s, const void *src, void *dst, uint64_t n16);
 
 namespace {
 
-constexpr int kSlots = 3;
+constexpr int kMaxSlots = 8;   // batches in flight: 3 by default, PPG_CURSOR_SLOTS overrides (2..8)
 
 struct Slot {
     ppg_shard sh;                       // device state of the batch (its own stream)
     DevBuf<uint8_t> dcomp;              // the batch's compressed bytes in HBM
     PinnedBuf pcomp;                    // ... staged in pinned host memory
     PinnedBuf text;                     // raw_k = offset_k ++ chunk_k, concatenated
+    DevBuf<uint8_t> dtext;              // ... packed on the device first (one D2H per batch)
+    DevBuf<int64_t> draw_off;
     PinnedBuf desc;                     // 4 x u32 per record
     std::vector<int64_t> raw_off, rec_off;
     int32_t b0 = 0, b1 = 0;             // chunks [b0, b1) relative to the cursor's first
@@ -53,13 +63,18 @@ struct ppg_cursor {
     int threads = 8;
     bool split = false;                 // batches smaller than ~6 generations of waves split at side points
     std::vector<std::pair<int32_t, int32_t>> batches;
-    Slot slot[kSlots];
+    Slot slot[kMaxSlots];
+    int nslots = 3;
+    // how a batch's text and descriptors reach the host: 2 (default) the pack kernel stores them
+    // straight into the pinned buffers; 1 packed on the device, one D2H copy; 0 one D2H copy per chunk
+    int pack = 2;
+    bool verbose = false;               // PPG_CURSOR_VERBOSE: per-batch stage times on stderr
     size_t next = 0;                    // next batch to hand out
     int64_t record_base = 0;
 
     ~ppg_cursor() {
         for (auto &s : slot)
-            if (s.worker.joinable()) s.worker.join();
+            if (s.worker.joinable()) s.worker.join();   // (slots past nslots never started)
         (void)hipSetDevice(ctx->device);
         for (auto &s : slot) {
             for (auto &e : s.sh.ev) if (e) (void)hipEventDestroy(e);
@@ -86,23 +101,31 @@ struct ppg_cursor {
     // every slot's buffers, once, for the largest batch (the shard's device buffers reach their
     // size with the first shard_prepare and are then reused: DevBuf::alloc keeps a large enough one)
     int size_slots() {
-        int64_t cmax = 1, rmax = 1;
+        int64_t cmax = 1, rmax = 1, max_chunks = 1;
         for (size_t i = 0; i < batches.size(); i++) {
+            max_chunks = std::max<int64_t>(max_chunks, batches[i].second - batches[i].first);
             cmax = std::max(cmax, comp_len(i));
             rmax = std::max(rmax, raw_len(i));
         }
-        for (auto &s : slot) {
+        for (int q = 0; q < nslots; q++) {
+            Slot &s = slot[q];
             HIPCHK(s.pcomp.alloc((size_t)cmax));
             HIPCHK(s.dcomp.alloc((size_t)cmax + 64));
             HIPCHK(s.text.alloc((size_t)rmax));
-            // descriptors: 16 B per record, for records of >= 64 B on average (grown only beyond)
-            HIPCHK(s.desc.alloc((size_t)(rmax / 4 + 4096)));
+            if (pack) HIPCHK(s.draw_off.alloc((size_t)max_chunks + 1));
+            if (pack == 1) HIPCHK(s.dtext.alloc((size_t)rmax));
+            // descriptors: 16 B per record, for records of >= 128 B on average (grown only beyond)
+            HIPCHK(s.desc.alloc((size_t)(rmax / 8 + 4096)));
         }
         return PPG_OK;
     }
 
     // read, decode and bring back batch i into slot s (runs on the slot's worker thread)
     int produce(size_t i, Slot &s) {
+        using Clk = std::chrono::steady_clock;
+        const auto t0 = Clk::now();
+        auto ms = [&] { return std::chrono::duration<double, std::milli>(Clk::now() - t0).count(); };
+        double tr = 0, tp = 0, td = 0;
         if (hipSetDevice(ctx->device) != hipSuccess) return PPG_DEVICE_ERROR;
         const auto &P = ix->pts;
         const int32_t a = first + batches[i].first, b = first + batches[i].second;
@@ -110,6 +133,7 @@ struct ppg_cursor {
         s.b1 = batches[i].second;
         const int64_t lo = P[(size_t)a].input - 1, len = comp_len(i);
         if (!pread_parallel(fd, s.pcomp.p, lo, len, threads)) return PPG_IO_ERROR;
+        tr = ms();
         hipStream_t st = s.sh.stream;
         HIPCHK(hipMemsetAsync(s.dcomp.p + len, 0, 64, st));
         HIPCHK(hipMemcpyAsync(s.dcomp.p, s.pcomp.p, (size_t)len, hipMemcpyHostToDevice, st));
@@ -117,10 +141,12 @@ struct ppg_cursor {
         if (split)
             if (int rc = shard_split_from_index(&s.sh, ix, a, b - a)) return rc;
         shard_reset(&s.sh);
-        float ms = 0;
+        tp = ms();
+        float kms = 0;
         if (int rc = batch_launch(&s.sh, 0, s.sh.n)) return rc;
-        if (int rc = batch_collect(&s.sh, 0, s.sh.n, ms)) return rc;
-        if (int rc = shard_finish(&s.sh, ms)) return rc;
+        if (int rc = batch_collect(&s.sh, 0, s.sh.n, kms)) return rc;
+        if (int rc = shard_finish(&s.sh, kms)) return rc;
+        td = ms();
         // raw_k = offset_k ++ chunk_k (Parsing.Parse's CombinedMemory), back to pinned host memory
         const int32_t m = b - a;
         s.raw_off.assign((size_t)m + 1, 0);
@@ -130,24 +156,47 @@ struct ppg_cursor {
         if ((size_t)s.raw_off[(size_t)m] > s.text.n) return PPG_BUF_ERROR;   // produced <= Output span: never
         s.nrec = s.sh.total_records;
         if ((size_t)(16 * s.nrec) > s.desc.n) HIPCHK(s.desc.alloc((size_t)(16 * s.nrec + (16 * s.nrec) / 4)));
-        // the chunks' bodies are contiguous on the device; each lands after its offset carry
-        for (int32_t k = 0; k < m; k++) {
-            const auto &off = P[(size_t)a + k].offset;
-            uint8_t *dst = s.text.p + s.raw_off[(size_t)k];
-            if (!off.empty()) memcpy(dst, off.data(), off.size());
-            const uint64_t got = s.sh.h_res[(size_t)k].produced;
-            if (got) HIPCHK(hipMemcpyAsync(dst + off.size(), s.sh.out.p + s.sh.h_jobs[(size_t)k].out_off, got,
-                                           hipMemcpyDeviceToHost, st));
+        if (pack == 2) {
+            // raw_k = offset_k ++ chunk_k stored by the pack kernel straight into the pinned text
+            // buffer, the descriptors likewise: the copy engines stay free for the host -> device
+            // direction of the other batches (SDMA copies of the two directions serialised, r03:
+            // tools/pcie_probe.hip)
+            HIPCHK(hipMemcpyAsync(s.draw_off.p, s.raw_off.data(), 8 * ((size_t)m + 1), hipMemcpyHostToDevice, st));
+            HIPCHK(ppg_launch_pack_raw(st, s.sh.out.p, s.sh.jobs.p, s.sh.res.p, s.sh.offs.p, s.sh.oref.p,
+                                       s.draw_off.p, s.text.p, m));
+            HIPCHK(ppg_launch_copy16(st, s.sh.recs.p, s.desc.p, (uint64_t)s.nrec));
+        } else if (pack == 1) {
+            // packed on the device, then the batch's text crosses PCIe as one copy
+            HIPCHK(hipMemcpyAsync(s.draw_off.p, s.raw_off.data(), 8 * ((size_t)m + 1), hipMemcpyHostToDevice, st));
+            HIPCHK(ppg_launch_pack_raw(st, s.sh.out.p, s.sh.jobs.p, s.sh.res.p, s.sh.offs.p, s.sh.oref.p,
+                                       s.draw_off.p, s.dtext.p, m));
+            if (s.raw_off[(size_t)m])
+                HIPCHK(hipMemcpyAsync(s.text.p, s.dtext.p, (size_t)s.raw_off[(size_t)m], hipMemcpyDeviceToHost, st));
+        } else {
+            // the chunks' bodies are contiguous on the device; each lands after its offset carry
+            // (one copy per chunk measured faster than packing + one copy: 98 vs 85 M records/s, r03)
+            for (int32_t k = 0; k < m; k++) {
+                const auto &off = P[(size_t)a + k].offset;
+                uint8_t *dst = s.text.p + s.raw_off[(size_t)k];
+                if (!off.empty()) memcpy(dst, off.data(), off.size());
+                const uint64_t got = s.sh.h_res[(size_t)k].produced;
+                if (got) HIPCHK(hipMemcpyAsync(dst + off.size(), s.sh.out.p + s.sh.h_jobs[(size_t)k].out_off, got,
+                                               hipMemcpyDeviceToHost, st));
+            }
         }
-        if (s.nrec) HIPCHK(hipMemcpyAsync(s.desc.p, s.sh.recs.p, 16 * (size_t)s.nrec, hipMemcpyDeviceToHost, st));
+        if (s.nrec && pack != 2)
+            HIPCHK(hipMemcpyAsync(s.desc.p, s.sh.recs.p, 16 * (size_t)s.nrec, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        if (verbose)
+            fprintf(stderr, "[cursor] batch %zu: %d chunks, read %.1f ms, H2D+prepare %.1f, decode %.1f (kernels %.1f), "
+                            "to host %.1f, total %.1f ms\n", i, m, tr, tp - tr, td - tp, (double)kms, ms() - td, ms());
         s.rec_off.assign((size_t)m + 1, 0);
         for (int32_t k = 0; k < m; k++) s.rec_off[(size_t)k + 1] = s.sh.h_base[(size_t)k] + (int64_t)s.sh.h_info[(size_t)k].records;
         return PPG_OK;
     }
 
     void start(size_t i) {
-        Slot &s = slot[i % kSlots];
+        Slot &s = slot[i % (size_t)nslots];
         s.rc = PPG_OK;
         s.worker = std::thread([this, i, &s] { s.rc = produce(i, s); });
     }
@@ -168,6 +217,9 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
     c->first = first;
     c->n = n;
     c->threads = threads > 0 ? threads : 8;
+    if (const char *e = getenv("PPG_CURSOR_SLOTS")) c->nslots = std::min(kMaxSlots, std::max(2, atoi(e)));
+    if (const char *e = getenv("PPG_CURSOR_PACK")) c->pack = std::min(2, std::max(0, atoi(e)));
+    c->verbose = getenv("PPG_CURSOR_VERBOSE") != nullptr;
     c->fd = open(gz_path, O_RDONLY);
     if (c->fd < 0) return PPG_IO_ERROR;
     // batches: whole chunks, at most batch_bytes of raw text each (at least one chunk)
@@ -192,12 +244,12 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
         HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
         c->split = (int64_t)max_chunks < 6 * 32 * (int64_t)cus;
     }
-    for (auto &s : c->slot) {
-        s.sh.ctx = ctx;
-        HIPCHK(hipStreamCreateWithFlags(&s.sh.stream, hipStreamNonBlocking));
+    for (int q = 0; q < c->nslots; q++) {
+        c->slot[q].sh.ctx = ctx;
+        HIPCHK(hipStreamCreateWithFlags(&c->slot[q].sh.stream, hipStreamNonBlocking));
     }
     if (int rc = c->size_slots()) return rc;
-    for (size_t i = 0; i < c->batches.size() && i < (size_t)kSlots - 1; i++) c->start(i);
+    for (size_t i = 0; i < c->batches.size() && i < (size_t)c->nslots - 1; i++) c->start(i);
     *out = c.release();
     return PPG_OK;
 }
@@ -205,14 +257,15 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
 int ppg_cursor_next(ppg_cursor *c, ppg_batch *b) {
     if (!c || !b) return PPG_ARG_ERROR;
     if (c->next >= c->batches.size()) return PPG_STREAM_END;
-    Slot &s = c->slot[c->next % kSlots];
+    const size_t S = (size_t)c->nslots;
+    Slot &s = c->slot[c->next % S];
     if (s.worker.joinable()) s.worker.join();
     if (s.rc != PPG_OK) return s.rc;
     // the slot of the batch handed out last time is free again: the caller is done with it
-    if (c->next + kSlots - 1 < c->batches.size()) {
-        Slot &f = c->slot[(c->next + kSlots - 1) % kSlots];
+    if (c->next + S - 1 < c->batches.size()) {
+        Slot &f = c->slot[(c->next + S - 1) % S];
         if (f.worker.joinable()) f.worker.join();
-        c->start(c->next + kSlots - 1);
+        c->start(c->next + S - 1);
     }
     b->first_chunk = c->first + s.b0;
     b->nchunks = s.b1 - s.b0;

@@ -544,6 +544,36 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
 #endif
 }
 
+// The walk two tokens per step (PPG_WALK_PAIR): vt2[c] is the token word of the candidate right
+// after c's token (c + bits(c)), gathered once per span by one ds_bpermute, so a step reads both
+// tokens at once and the walk's serial chain -- v_readlane -> s_add -> v_readlane, ~75 cycles per
+// token on gfx950 even for a wave alone on its SIMD (tools/walk_lat.hip) -- is paid once per two
+// tokens.  The first token is placed and tested as before; a step whose first token already ends
+// the walk leaves without placing the second (its lane select would wrap), so X, the placed tokens
+// and the stop are exactly walk_asm's.
+template <uint32_t STOPMASK = 0x1C0C0u>
+__device__ __forceinline__ void walk_asm_pair(uint32_t vt, uint32_t vt2, uint32_t &vtin, uint32_t &X) {
+    uint32_t t, u, tmp;
+    asm volatile(
+        "1:\n\t"
+        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
+        "v_readlane_b32 %[u], %[vt2], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], %[M]\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[u], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], %[M]\n\t"
+        "v_writelane_b32 %[vtin], %[u], m0\n\t"
+        "s_cbranch_scc0 1b\n"
+        "2:"
+        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [u] "=&s"(u), [tmp] "=&s"(tmp)
+        : [vt] "v"(vt), [vt2] "v"(vt2), [M] "i"(STOPMASK)
+        : "m0", "scc");
+}
+
 // IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
 // IX = true:  CreateIndex pass 1 (ppg_index_gpu.cpp): decode whole blocks from a candidate block
 //             start until a block ends at or past stop_bit, recording every block end.
@@ -863,6 +893,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                         asm volatile("s_setprio " PPG_STR(PPG_POST_WALK_PRIO));
 #endif
                         return Round{vtin, off, (X & 255u) - (sp2 ? 128u : 0u), sp2};
+                    }
+#elif defined(PPG_WALK_PAIR)
+                    {
+                        // each candidate's following token (wraps past lane 63: such a first token
+                        // ends the span, so the second is never used)
+                        const uint32_t vta2 = bperm(((uint32_t)lane + (vta & 255u)) << 2, vta);
+                        const uint32_t vtb2 = bperm(((uint32_t)lane + (vtb & 255u)) << 2, vtb);
+                        walk_asm_pair(vta, vta2, vtin, X);
+                        if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
+                            X -= 64;
+                            half = 64;
+                            walk_asm_pair(vtb, vtb2, vtin, X);
+                        }
                     }
 #else
                     walk_asm(vta, vtin, X);
