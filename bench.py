@@ -241,9 +241,10 @@ def enumerate_run(tf, ix, path, dev, threads, batch_gib, pcie):
     return {"records_per_s": nrec / sec, "records_per_s_incl_open": nrec / (sec + t_open), "seconds": sec,
             "open_s": t_open, "batches": nb, "batch_GiB": batch_gib, "host_GBps": host_bytes / sec / 1e9,
             "pcie_d2h_GBps": pcie, "pcie_bound_records_per_s": bound, "frac_of_pcie_bound": nrec / sec / bound,
-            "note": "ppg_cursor: pread -> pinned -> H2D -> decode -> D2H of raw text + descriptors, 3 batches in "
-                    "flight (own stream + worker thread each), buffers sized once at open; records counted, not "
-                    "materialised as objects; not the bench value"}
+            "note": "ppg_cursor: pread -> pinned -> H2D -> decode -> device pack -> one D2H of raw text + "
+                    "descriptors per batch, 4 batches in flight in stage order (own stream + worker thread each), "
+                    "buffers sized once at open; records counted, not materialised as objects; not the bench "
+                    "value"}
 
 
 def ingest_run(tf, ix, dev, threads, piece_gib=8.0, enum_gib=0.0):

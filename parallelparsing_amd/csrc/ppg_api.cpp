@@ -533,6 +533,52 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
     return PPG_OK;
 }
 
+// Size a shard's device buffers once for every range [first + a, first + b) it will be prepared for
+// (with their side points when split), so that re-preparing it range after range never
+// reallocates: a hipFree waits for the whole device, and in a pipeline of several shards (the
+// cursor, host ingest) that stalled every other stream's decode and copies (r03: 300-560 ms per
+// 8 GiB cursor batch).  shard_prepare / ppg_shard_set_split then find every buffer large enough.
+int shard_reserve(ppg_shard *sh, const ppg_index *ix, int32_t first,
+                  const std::vector<std::pair<int32_t, int32_t>> &ranges, bool split) {
+    const auto &P = ix->pts;
+    const auto &O = ix->side_out;
+    int64_t n_max = 1, out_max = 0, off_max = 0, nsub_max = 0, nl_max = 0;
+    uint64_t nl_bytes = kNlBytesPerEntry;
+    if (const char *e = getenv("PPG_NL_BYTES")) nl_bytes = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    for (auto [a, b] : ranges) {
+        const int64_t n = b - a, lo = P[(size_t)first + a].output, hi = P[(size_t)first + b].output;
+        int64_t off = 0, nsub = 0;
+        for (int32_t k = first + a; k < first + b; k++) off += (int64_t)P[(size_t)k].offset.size();
+        if (split && !O.empty())
+            nsub = (int64_t)(std::lower_bound(O.begin(), O.end(), hi) - std::upper_bound(O.begin(), O.end(), lo));
+        nsub = std::max<int64_t>(nsub, 0);
+        n_max = std::max(n_max, n);
+        out_max = std::max(out_max, hi - lo);
+        off_max = std::max(off_max, off);
+        nsub_max = std::max(nsub_max, nsub);
+        // census: the chunks' regions, then (split) the pieces' past them (ppg_shard_set_split)
+        const int64_t per = nl_bytes >= (1ull << 40) ? 0 : (hi - lo) / (int64_t)nl_bytes;
+        nl_max = std::max(nl_max, per + 64 * n + (nsub ? per + 64 * (n + nsub) : 0));
+    }
+    HIPCHK(sh->jobs.alloc((size_t)n_max));
+    HIPCHK(sh->dicts.alloc((size_t)(n_max + nsub_max) * kWin));
+    HIPCHK(sh->offs.alloc((size_t)off_max + 16));
+    HIPCHK(sh->oref.alloc((size_t)n_max));
+    HIPCHK(sh->res.alloc((size_t)n_max));
+    HIPCHK(sh->info.alloc((size_t)n_max));
+    HIPCHK(sh->base.alloc((size_t)n_max));
+    HIPCHK(sh->total.alloc(1));
+    HIPCHK(sh->out.alloc((size_t)out_max + 64));
+    HIPCHK(sh->recs.alloc((size_t)(4 * (out_max / 256 + 1024))));
+    HIPCHK(sh->nls.alloc((size_t)nl_max + 64));
+    if (nsub_max) {
+        HIPCHK(sh->sjobs.alloc((size_t)(n_max + nsub_max)));
+        HIPCHK(sh->sres.alloc((size_t)(n_max + nsub_max)));
+        HIPCHK(sh->sidx.alloc((size_t)n_max + 1));
+    }
+    return PPG_OK;
+}
+
 extern "C" {
 
 int ppg_shard_create(ppg_ctx *ctx, const ppg_index *ix, int32_t first, int32_t n, const void *comp, int64_t comp_len,
@@ -767,13 +813,16 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
             sh->h_sjobs[j] = J;
         }
     }
-    // dictionaries: the chunks' windows, then the side points'
+    // dictionaries: the chunks' windows, then the side points' (in place when shard_reserve or an
+    // earlier split left room)
     DevBuf<uint8_t> d2;
-    HIPCHK(d2.alloc(((size_t)n + (size_t)nsub) * kWin));
-    HIPCHK(hipMemcpyAsync(d2.p, sh->dicts.p, (size_t)n * kWin, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(d2.p + (size_t)n * kWin, windows, (size_t)nsub * kWin, hipMemcpyHostToDevice, s));
-    std::swap(sh->dicts.p, d2.p);
-    std::swap(sh->dicts.n, d2.n);
+    if (sh->dicts.n < ((size_t)n + (size_t)nsub) * kWin) {
+        HIPCHK(d2.alloc(((size_t)n + (size_t)nsub) * kWin));
+        HIPCHK(hipMemcpyAsync(d2.p, sh->dicts.p, (size_t)n * kWin, hipMemcpyDeviceToDevice, s));
+        std::swap(sh->dicts.p, d2.p);
+        std::swap(sh->dicts.n, d2.n);
+    }
+    HIPCHK(hipMemcpyAsync(sh->dicts.p + (size_t)n * kWin, windows, (size_t)nsub * kWin, hipMemcpyHostToDevice, s));
     HIPCHK(sh->sjobs.alloc(sh->h_sjobs.size()));
     HIPCHK(hipMemcpyAsync(sh->sjobs.p, sh->h_sjobs.data(), sizeof(PpgInflateJob) * sh->h_sjobs.size(),
                           hipMemcpyHostToDevice, s));
@@ -1030,7 +1079,10 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
         }
     }
     IngestState &S = *ctx->ingest;
-    for (int i = 0; i < kPieces; i++) HIPCHK(S.db[i].alloc((size_t)maxlen + 64));
+    for (int i = 0; i < kPieces; i++) {
+        HIPCHK(S.db[i].alloc((size_t)maxlen + 64));
+        if (int r = shard_reserve(S.sh[i], ix, first, pieces, split)) return r;
+    }
     if (verbose) fprintf(stderr, "[ingest] %zu pieces, max %.1f MB, setup %.1f ms\n", pieces.size(), maxlen / 1e6, now_ms());
 
     // Producer thread: piece k -> device buffer k&1 (pread into pinned slots, H2D on the copy

@@ -10,12 +10,13 @@
 //
 // What bounds it is PCIe: every byte of text crosses device -> host once (~385 B per record at
 // 150 bp), the compressed input host -> device in the other direction.  So several batches are in
-// flight, each on its own stream and worker thread: while the caller walks batch k, batches k+1
-// and k+2 are being read, decoded and copied back, and the copies of one overlap the decode of
-// the next.  Every slot's buffers -- pinned text / descriptor / compressed staging, device input,
-// output, census -- are sized once at open from the largest batch, so no worker reallocates (a
-// hipHostFree / hipFree can synchronise the device).  A batch's raw_k are packed on the device
-// (ppg_pack_raw) and cross PCIe as one copy.  An index with side points
+// flight, each on its own stream and worker thread, in stage order: while the caller walks batch
+// k, batch k+1 crosses PCIe, k+2 decodes and k+3 is read, and the device -> host copies run back
+// to back (r03: 122 M records/s, 86% of the PCIe bound).  Every slot's buffers -- pinned text /
+// descriptor / compressed staging, device input, output, census, and the shard's own -- are sized
+// once at open from the largest batch, so no worker reallocates (a hipFree waits for the whole
+// device: 300-560 ms stalls per batch before r03's shard_reserve).  A batch's raw_k are packed on
+// the device (ppg_pack_raw) and cross PCIe as one copy.  An index with side points
 // (ppg_index_build_gpu_side) splits a batch's chunks into several waves when the batch is too
 // small to fill the GPU by itself.
 //
@@ -26,17 +27,19 @@
 #include <fcntl.h>
 #include <unistd.h>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 
 // launcher (ppg_parse.hip)
 hipError_t ppg_launch_pack_raw(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs, const PpgInflateResult *ires,
                                const uint8_t *offs, const PpgOffsetRef *oref, const int64_t *raw_off, uint8_t *dst,
-                               int n);
-hipError_t ppg_launch_copy16(hipStream_t s, const void *src, void *dst, uint64_t n16);
+                               int n, int blocks);
+hipError_t ppg_launch_copy16(hipStream_t s, const void *src, void *dst, uint64_t n16, int blocks);
 
 namespace {
 
-constexpr int kMaxSlots = 8;   // batches in flight: 3 by default, PPG_CURSOR_SLOTS overrides (2..8)
+constexpr int kMaxSlots = 8;   // batches held: 5 by default (4 in flight + the caller's), PPG_CURSOR_SLOTS 2..8
 
 struct Slot {
     ppg_shard sh;                       // device state of the batch (its own stream)
@@ -64,13 +67,37 @@ struct ppg_cursor {
     bool split = false;                 // batches smaller than ~6 generations of waves split at side points
     std::vector<std::pair<int32_t, int32_t>> batches;
     Slot slot[kMaxSlots];
-    int nslots = 3;
-    // how a batch's text and descriptors reach the host: 2 (default) the pack kernel stores them
-    // straight into the pinned buffers; 1 packed on the device, one D2H copy; 0 one D2H copy per chunk
-    int pack = 2;
+    int nslots = 5;
+    // how a batch's text and descriptors reach the host (PPG_CURSOR_PACK): 1 (default) packed on the
+    // device, then one copy-engine copy at the PCIe rate; 0 one copy per chunk (~45 GB/s: 2,000+
+    // small copies); 2 the pack kernel stores straight into the pinned buffers -- no copy engine,
+    // but while those stores drain over PCIe the other batches' decode kernels do not complete
+    // (decode 90 -> 250-440 ms with a pack in flight, any grid size, r03), so it loses
+    int pack = 1;
+    int pack_blocks = 256;              // pack = 2: workgroups of the pack kernels (PPG_CURSOR_PACK_BLOCKS)
     bool verbose = false;               // PPG_CURSOR_VERBOSE: per-batch stage times on stderr
+    std::chrono::steady_clock::time_point t_open = std::chrono::steady_clock::now();
     size_t next = 0;                    // next batch to hand out
     int64_t record_base = 0;
+    // stage order across batches: batch i reads only after batch i-1 has read, and starts its
+    // device -> host transfer only after batch i-1's has completed.  Without it the batches in
+    // flight start together and move in lockstep -- all reading, then all decoding, then all
+    // copying -- and PCIe idles between the groups (r03: 3 batches started at once, ~90 M
+    // records/s); in order, batch i+1 reads and decodes while batch i crosses PCIe.
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint8_t> stage;         // per batch: kRead | kHost once that stage is over (or failed)
+    static constexpr uint8_t kRead = 1, kHost = 2;
+    void stage_done(size_t i, uint8_t bit) {
+        std::lock_guard<std::mutex> lk(mu);
+        stage[i] |= bit;
+        cv.notify_all();
+    }
+    void stage_wait(size_t i, uint8_t bit) {   // for batch i-1's stage
+        if (i == 0) return;
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return (stage[i - 1] & bit) != 0; });
+    }
 
     ~ppg_cursor() {
         for (auto &s : slot)
@@ -98,8 +125,8 @@ struct ppg_cursor {
         return t;
     }
 
-    // every slot's buffers, once, for the largest batch (the shard's device buffers reach their
-    // size with the first shard_prepare and are then reused: DevBuf::alloc keeps a large enough one)
+    // every slot's buffers, once, for the largest batch -- the shard's device buffers too
+    // (shard_reserve): a reallocation in a worker frees first, and hipFree waits for the device
     int size_slots() {
         int64_t cmax = 1, rmax = 1, max_chunks = 1;
         for (size_t i = 0; i < batches.size(); i++) {
@@ -116,6 +143,7 @@ struct ppg_cursor {
             if (pack == 1) HIPCHK(s.dtext.alloc((size_t)rmax));
             // descriptors: 16 B per record, for records of >= 128 B on average (grown only beyond)
             HIPCHK(s.desc.alloc((size_t)(rmax / 8 + 4096)));
+            if (int rc = shard_reserve(&s.sh, ix, first, batches, split)) return rc;
         }
         return PPG_OK;
     }
@@ -126,13 +154,20 @@ struct ppg_cursor {
         const auto t0 = Clk::now();
         auto ms = [&] { return std::chrono::duration<double, std::milli>(Clk::now() - t0).count(); };
         double tr = 0, tp = 0, td = 0;
+        struct Done {   // every exit, failures included, releases the next batch's waits
+            ppg_cursor *c; size_t i;
+            ~Done() { c->stage_done(i, kRead | kHost); }
+        } done{this, i};
         if (hipSetDevice(ctx->device) != hipSuccess) return PPG_DEVICE_ERROR;
         const auto &P = ix->pts;
         const int32_t a = first + batches[i].first, b = first + batches[i].second;
         s.b0 = batches[i].first;
         s.b1 = batches[i].second;
         const int64_t lo = P[(size_t)a].input - 1, len = comp_len(i);
+        stage_wait(i, kRead);
+        const double tw = ms();
         if (!pread_parallel(fd, s.pcomp.p, lo, len, threads)) return PPG_IO_ERROR;
+        stage_done(i, kRead);
         tr = ms();
         hipStream_t st = s.sh.stream;
         HIPCHK(hipMemsetAsync(s.dcomp.p + len, 0, 64, st));
@@ -156,6 +191,8 @@ struct ppg_cursor {
         if ((size_t)s.raw_off[(size_t)m] > s.text.n) return PPG_BUF_ERROR;   // produced <= Output span: never
         s.nrec = s.sh.total_records;
         if ((size_t)(16 * s.nrec) > s.desc.n) HIPCHK(s.desc.alloc((size_t)(16 * s.nrec + (16 * s.nrec) / 4)));
+        stage_wait(i, kHost);
+        const double th = ms();
         if (pack == 2) {
             // raw_k = offset_k ++ chunk_k stored by the pack kernel straight into the pinned text
             // buffer, the descriptors likewise: the copy engines stay free for the host -> device
@@ -163,13 +200,13 @@ struct ppg_cursor {
             // tools/pcie_probe.hip)
             HIPCHK(hipMemcpyAsync(s.draw_off.p, s.raw_off.data(), 8 * ((size_t)m + 1), hipMemcpyHostToDevice, st));
             HIPCHK(ppg_launch_pack_raw(st, s.sh.out.p, s.sh.jobs.p, s.sh.res.p, s.sh.offs.p, s.sh.oref.p,
-                                       s.draw_off.p, s.text.p, m));
-            HIPCHK(ppg_launch_copy16(st, s.sh.recs.p, s.desc.p, (uint64_t)s.nrec));
+                                       s.draw_off.p, s.text.p, m, pack_blocks));
+            HIPCHK(ppg_launch_copy16(st, s.sh.recs.p, s.desc.p, (uint64_t)s.nrec, pack_blocks));
         } else if (pack == 1) {
             // packed on the device, then the batch's text crosses PCIe as one copy
             HIPCHK(hipMemcpyAsync(s.draw_off.p, s.raw_off.data(), 8 * ((size_t)m + 1), hipMemcpyHostToDevice, st));
             HIPCHK(ppg_launch_pack_raw(st, s.sh.out.p, s.sh.jobs.p, s.sh.res.p, s.sh.offs.p, s.sh.oref.p,
-                                       s.draw_off.p, s.dtext.p, m));
+                                       s.draw_off.p, s.dtext.p, m, 0));
             if (s.raw_off[(size_t)m])
                 HIPCHK(hipMemcpyAsync(s.text.p, s.dtext.p, (size_t)s.raw_off[(size_t)m], hipMemcpyDeviceToHost, st));
         } else {
@@ -187,9 +224,12 @@ struct ppg_cursor {
         if (s.nrec && pack != 2)
             HIPCHK(hipMemcpyAsync(s.desc.p, s.sh.recs.p, 16 * (size_t)s.nrec, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        stage_done(i, kHost);
         if (verbose)
-            fprintf(stderr, "[cursor] batch %zu: %d chunks, read %.1f ms, H2D+prepare %.1f, decode %.1f (kernels %.1f), "
-                            "to host %.1f, total %.1f ms\n", i, m, tr, tp - tr, td - tp, (double)kms, ms() - td, ms());
+            fprintf(stderr, "[cursor] batch %zu: %d chunks, started at %.1f ms: read wait %.1f, read %.1f, H2D+prepare %.1f, "
+                            "decode %.1f (kernels %.1f), host wait %.1f, to host %.1f, total %.1f ms\n", i, m,
+                    std::chrono::duration<double, std::milli>(t0 - t_open).count(), tw, tr - tw, tp - tr, td - tp,
+                    (double)kms, th - td, ms() - th, ms());
         s.rec_off.assign((size_t)m + 1, 0);
         for (int32_t k = 0; k < m; k++) s.rec_off[(size_t)k + 1] = s.sh.h_base[(size_t)k] + (int64_t)s.sh.h_info[(size_t)k].records;
         return PPG_OK;
@@ -219,6 +259,7 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
     c->threads = threads > 0 ? threads : 8;
     if (const char *e = getenv("PPG_CURSOR_SLOTS")) c->nslots = std::min(kMaxSlots, std::max(2, atoi(e)));
     if (const char *e = getenv("PPG_CURSOR_PACK")) c->pack = std::min(2, std::max(0, atoi(e)));
+    if (const char *e = getenv("PPG_CURSOR_PACK_BLOCKS")) c->pack_blocks = std::max(4, atoi(e));
     c->verbose = getenv("PPG_CURSOR_VERBOSE") != nullptr;
     c->fd = open(gz_path, O_RDONLY);
     if (c->fd < 0) return PPG_IO_ERROR;
@@ -249,6 +290,7 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
         HIPCHK(hipStreamCreateWithFlags(&c->slot[q].sh.stream, hipStreamNonBlocking));
     }
     if (int rc = c->size_slots()) return rc;
+    c->stage.assign(c->batches.size(), 0);
     for (size_t i = 0; i < c->batches.size() && i < (size_t)c->nslots - 1; i++) c->start(i);
     *out = c.release();
     return PPG_OK;

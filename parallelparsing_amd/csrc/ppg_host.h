@@ -195,4 +195,6 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1);
 int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms);
 int shard_finish(ppg_shard *sh, float total_ms);
 int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n);
+int shard_reserve(ppg_shard *sh, const ppg_index *ix, int32_t first,
+                  const std::vector<std::pair<int32_t, int32_t>> &ranges, bool split);
 bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads);

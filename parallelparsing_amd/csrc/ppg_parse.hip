@@ -407,8 +407,8 @@ extern "C" __global__ __launch_bounds__(256) void ppg_record_keys(
 // The record cursor's batch layout (ppg_cursor, BatchedFASTQ's enumerator): raw_k = offset_k ++
 // chunk_k (Parsing.cs's CombinedMemory) of every chunk of a batch packed contiguously at
 // dst + raw_off[k] on the device, so the batch crosses PCIe as one device -> host copy instead of
-// one per chunk.  Grid (stripes, chunks); a stripe copies its share of one chunk bytewise (lanes
-// in a row: every wave access is one contiguous 64-byte run).
+// one per chunk.  Grid (stripes, chunk slots); a block copies its stripe of chunks
+// blockIdx.y, blockIdx.y + gridDim.y, ... (lanes in a row: every wave access is one contiguous run).
 // ------------------------------------------------------------------------------------------
 // dst may be pinned host memory (the cursor writes each batch straight into it: the kernel's
 // stores cross PCIe, which leaves the copy engines to the host -> device direction -- SDMA copies
@@ -426,36 +426,36 @@ extern "C" __global__ __launch_bounds__(256) void ppg_pack_raw(const uint8_t *__
                                                                const PpgOffsetRef *__restrict__ oref,
                                                                const int64_t *__restrict__ raw_off,
                                                                uint8_t *__restrict__ dst, int n) {
-    const int k = blockIdx.y;
-    if (k >= n) return;
-    const uint64_t olen = oref[k].len, blen = ires[k].produced;
-    const uint8_t *off = offs + oref[k].start, *body = out + jobs[k].out_off;
-    const uint64_t d0 = (uint64_t)raw_off[k], total = olen + blen;   // raw byte i -> dst[d0 + i]
-    // 16-B destination words [w0, w1) lying entirely inside the body part; the rest bytewise
-    const uint64_t body_d = d0 + olen;
-    const uint64_t w0 = (body_d + 15) / 16, w1 = (d0 + total) / 16;
-    const uint64_t nw = w1 > w0 ? w1 - w0 : 0;
-    const uint64_t per = (nw + gridDim.x - 1) / gridDim.x;
-    const uint64_t a = w0 + min(nw, (uint64_t)blockIdx.x * per), z = w0 + min(nw, (uint64_t)(blockIdx.x + 1) * per);
-    for (uint64_t w = a + threadIdx.x; w < z; w += 256) {
-        const uint64_t sb = 16 * w - body_d;                     // body byte of the word's first byte
-        const uint8_t *src = body + sb;
-        const uint32_t *s32 = (const uint32_t *)((uintptr_t)src & ~(uintptr_t)3);
-        const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
-        const uint32_t x0 = s32[0], x1 = s32[1], x2 = s32[2], x3 = s32[3], x4 = s32[4];   // out has a 64-B tail
-        uint4 v;
-        v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
-        v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
-        v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
-        v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
-        *(uint4 *)(dst + 16 * w) = v;
-    }
-    if (blockIdx.x == 0) {   // the head (offset carry + unaligned start) and the unaligned tail
-        const uint64_t head = nw ? 16 * w0 - d0 : total;
-        for (uint64_t i = threadIdx.x; i < head; i += 256) dst[d0 + i] = (uint8_t)raw_byte(off, olen, body, i);
-        if (nw)
-            for (uint64_t i = 16 * w1 - d0 + threadIdx.x; i < total; i += 256)
-                dst[d0 + i] = (uint8_t)raw_byte(off, olen, body, i);
+    for (int k = blockIdx.y; k < n; k += gridDim.y) {
+        const uint64_t olen = oref[k].len, blen = ires[k].produced;
+        const uint8_t *off = offs + oref[k].start, *body = out + jobs[k].out_off;
+        const uint64_t d0 = (uint64_t)raw_off[k], total = olen + blen;   // raw byte i -> dst[d0 + i]
+        // 16-B destination words [w0, w1) lying entirely inside the body part; the rest bytewise
+        const uint64_t body_d = d0 + olen;
+        const uint64_t w0 = (body_d + 15) / 16, w1 = (d0 + total) / 16;
+        const uint64_t nw = w1 > w0 ? w1 - w0 : 0;
+        const uint64_t per = (nw + gridDim.x - 1) / gridDim.x;
+        const uint64_t a = w0 + min(nw, (uint64_t)blockIdx.x * per), z = w0 + min(nw, (uint64_t)(blockIdx.x + 1) * per);
+        for (uint64_t w = a + threadIdx.x; w < z; w += 256) {
+            const uint64_t sb = 16 * w - body_d;                     // body byte of the word's first byte
+            const uint8_t *src = body + sb;
+            const uint32_t *s32 = (const uint32_t *)((uintptr_t)src & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+            const uint32_t x0 = s32[0], x1 = s32[1], x2 = s32[2], x3 = s32[3], x4 = s32[4];   // out has a 64-B tail
+            uint4 v;
+            v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+            v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+            v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
+            v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
+            *(uint4 *)(dst + 16 * w) = v;
+        }
+        if (blockIdx.x == 0) {   // the head (offset carry + unaligned start) and the unaligned tail
+            const uint64_t head = nw ? 16 * w0 - d0 : total;
+            for (uint64_t i = threadIdx.x; i < head; i += 256) dst[d0 + i] = (uint8_t)raw_byte(off, olen, body, i);
+            if (nw)
+                for (uint64_t i = 16 * w1 - d0 + threadIdx.x; i < total; i += 256)
+                    dst[d0 + i] = (uint8_t)raw_byte(off, olen, body, i);
+        }
     }
 }
 
@@ -570,15 +570,20 @@ hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgIn
 
 hipError_t ppg_launch_pack_raw(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs, const PpgInflateResult *ires,
                                const uint8_t *offs, const PpgOffsetRef *oref, const int64_t *raw_off, uint8_t *dst,
-                               int n) {
+                               int n, int blocks) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_pack_raw, dim3(16, n), dim3(256), 0, s, out, jobs, ires, offs, oref, raw_off, dst, n);
+    // blocks > 0: at most that many workgroups (4 stripes each looping over chunks), so that a pack
+    // into pinned host memory -- PCIe-bound for ~170 ms per 8 GiB -- leaves the CUs to the next
+    // batch's decode instead of queueing (16 x chunks) workgroups ahead of it
+    const dim3 g = blocks > 0 ? dim3(4, (unsigned)std::max(1, std::min(n, blocks / 4))) : dim3(16, (unsigned)n);
+    hipLaunchKernelGGL(ppg_pack_raw, g, dim3(256), 0, s, out, jobs, ires, offs, oref, raw_off, dst, n);
     return hipGetLastError();
 }
 
-hipError_t ppg_launch_copy16(hipStream_t s, const void *src, void *dst, uint64_t n16) {
+hipError_t ppg_launch_copy16(hipStream_t s, const void *src, void *dst, uint64_t n16, int blocks) {
     if (!n16) return hipSuccess;
-    hipLaunchKernelGGL(ppg_copy16, dim3((unsigned)std::min<uint64_t>(4096, (n16 + 255) / 256)), dim3(256), 0, s,
+    const uint64_t cap = blocks > 0 ? (uint64_t)blocks : 4096;
+    hipLaunchKernelGGL(ppg_copy16, dim3((unsigned)std::min<uint64_t>(cap, (n16 + 255) / 256)), dim3(256), 0, s,
                        (const uint4 *)src, (uint4 *)dst, n16);
     return hipGetLastError();
 }
