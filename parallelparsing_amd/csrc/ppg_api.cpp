@@ -368,6 +368,7 @@ void ppg_close(ppg_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     ingest_free(ctx->ingest);
+    if (ctx->stage) (void)hipHostFree(ctx->stage);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

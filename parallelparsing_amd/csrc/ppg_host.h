@@ -105,6 +105,8 @@ struct ppg_ctx {
     int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
     int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)
     double ix_stats[kIxStats] = {0};   // timings / counts of the last GPU CreateIndex (ppg_index_build_gpu_stats)
+    uint8_t *stage = nullptr;           // pinned device -> host staging (CreateIndex windows), kept across calls
+    size_t stage_n = 0;
 };
 
 template <class T>

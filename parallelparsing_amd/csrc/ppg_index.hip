@@ -170,7 +170,33 @@ __global__ __launch_bounds__(256) void ppg_gather_kernel(const uint8_t *__restri
 
 // '@' census of out[s.lo, s.hi) per block (Core.cs:79-96): count, first and last '@' (relative to
 // lo) and the largest distance between consecutive '@' inside the block (SURVEY Q4 needs the
-// gaps).  One wave per block, 16 bytes per lane per step.
+// gaps).  One wave per block, 16 bytes per lane per 1 KiB step, four steps' loads issued together;
+// the "last '@' so far" prefix maximum is a DPP scan (r03: six ds_bpermute-based shuffles per step
+// held the kernel at ~2.3 TB/s).
+__device__ __forceinline__ uint32_t at_mask16(uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t x = w[j] ^ 0x40404040u;   // '@' bytes -> 0
+        const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+        m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * j);
+    }
+    return m;
+}
+
+// inclusive prefix maximum over the wave (DPP row shifts + row broadcasts, GFX9 encodings); lanes
+// without a source take -1
+__device__ __forceinline__ int32_t wave_incl_max(int32_t x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));   // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));   // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));   // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));   // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return x;
+}
+
 __global__ __launch_bounds__(64) void ppg_at_stats_kernel(const uint8_t *__restrict__ out,
                                                           const PpgSpan *__restrict__ spans, PpgAtStats *st, int n) {
     const int k = blockIdx.x;
@@ -179,49 +205,40 @@ __global__ __launch_bounds__(64) void ppg_at_stats_kernel(const uint8_t *__restr
     const uint64_t a = spans[k].lo, b = spans[k].hi;
     uint32_t cnt = 0, gmax = 0;
     int32_t first = 0x7FFFFFFF, carry = -1;   // carry: last '@' so far (relative), -1 none
-    for (uint64_t g0 = a & ~15ull; g0 < b; g0 += 1024) {
-        const uint64_t q = g0 + 16ull * (uint64_t)lane;
-        uint32_t m = 0;
-        if (q < b) {
-            const uint4 v = *(const uint4 *)(out + q);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (uint64_t g0 = a & ~15ull; g0 < b; g0 += 4096) {
+        uint4 v[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t x = w[j] ^ 0x40404040u;   // '@' bytes -> 0
-                const uint32_t t = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-                m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * j);
+        for (int i = 0; i < 4; i++) {
+            const uint64_t q = g0 + 1024ull * i + 16ull * (uint64_t)lane;
+            v[i] = q < b ? *(const uint4 *)(out + q) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t q = g0 + 1024ull * i + 16ull * (uint64_t)lane;
+            uint32_t m = q < b ? at_mask16(v[i]) : 0u;
+            if (q < a) m &= 0xFFFFu << (uint32_t)(a - q);   // lane 0 of the first step only
+            if (q < b && q + 16 > b) m &= (1u << (uint32_t)(b - q)) - 1u;
+            const int32_t rel = (int32_t)(q - a);
+            const int32_t f = m ? rel + __builtin_ctz(m) : 0x7FFFFFFF;
+            const int32_t l = m ? rel + 31 - __builtin_clz(m) : -1;
+            // gaps between consecutive '@' of this lane's 16 bytes
+            uint32_t mm = m, lg = 0;
+            int32_t prev = -1;
+            while (mm) {
+                const int32_t j = __builtin_ctz(mm);
+                if (prev >= 0) lg = max(lg, (uint32_t)(j - prev));
+                prev = j;
+                mm &= mm - 1;
             }
-            // bytes outside [a, b)
-            if (q < a) m &= 0xFFFFu << (uint32_t)(a - q);
-            if (q + 16 > b) m &= (1u << (uint32_t)(b - q)) - 1u;
+            // last '@' before this lane's bytes: prefix max over lower lanes, then the carry
+            const int32_t incl = wave_incl_max(l);
+            const int32_t excl = max(__builtin_amdgcn_update_dpp(-1, incl, 0x138, 0xF, 0xF, false), carry);   // wave_shr:1
+            if (m && excl >= 0) lg = max(lg, (uint32_t)(f - excl));
+            gmax = max(gmax, lg);
+            carry = max(carry, __builtin_amdgcn_readlane(incl, 63));
+            cnt += (uint32_t)__builtin_popcount(m);
+            first = min(first, f);
         }
-        const int32_t rel = (int32_t)(q - a);
-        const int32_t f = m ? rel + __builtin_ctz(m) : 0x7FFFFFFF;
-        const int32_t l = m ? rel + 31 - __builtin_clz(m) : -1;
-        // gaps between consecutive '@' of this lane's 16 bytes
-        uint32_t mm = m, lg = 0;
-        int32_t prev = -1;
-        while (mm) {
-            const int32_t i = __builtin_ctz(mm);
-            if (prev >= 0) lg = max(lg, (uint32_t)(i - prev));
-            prev = i;
-            mm &= mm - 1;
-        }
-        // last '@' before this lane's bytes: prefix max over lower lanes, then the carry
-        int32_t incl = l;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int32_t y = __shfl_up(incl, d);
-            if (lane >= d) incl = max(incl, y);
-        }
-        int32_t excl = __shfl_up(incl, 1);
-        if (lane == 0) excl = -1;
-        excl = max(excl, carry);
-        if (m && excl >= 0) lg = max(lg, (uint32_t)(f - excl));
-        gmax = max(gmax, lg);
-        carry = max(carry, __shfl(incl, 63));
-        cnt += (uint32_t)__builtin_popcount(m);
-        first = min(first, f);
     }
     for (int d = 32; d >= 1; d >>= 1) {
         cnt += __shfl_xor(cnt, d);

@@ -36,8 +36,11 @@
 #include <zlib.h>
 #include <chrono>
 #include <cstdlib>
+#include <algorithm>
 #include <memory>
+#include <thread>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
@@ -74,6 +77,52 @@ uint32_t spare_slots() {
 
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// device -> pageable host through the ctx's pinned staging buffer (two halves: the copy engine
+// fills one while host threads fan the other out).  A direct pageable copy of a batch's windows
+// (~860 MB) ran at ~10 GB/s, and at ~0.5 GB/s when the index's freshly grown pages were first
+// touched by it (r03: 1.6 s in one run of two).
+int copy_d2h_staged(ppg_ctx *ctx, hipStream_t s, uint8_t *dst, const uint8_t *src, size_t n) {
+    constexpr size_t kHalf = 128ull << 20;
+    constexpr int kThreads = 8;
+    if (!n) return PPG_OK;
+    if (!ctx->stage) {
+        HIPCHK(hipHostMalloc((void **)&ctx->stage, 2 * kHalf, hipHostMallocDefault));
+        ctx->stage_n = 2 * kHalf;
+    }
+    auto fan_out = [&](uint8_t *d, const uint8_t *h, size_t m) {
+        std::thread th[kThreads];
+        const size_t part = (m + kThreads - 1) / kThreads;
+        for (int t = 0; t < kThreads; t++) {
+            const size_t a = std::min(m, t * part), b = std::min(m, a + part);
+            th[t] = std::thread([=] { if (b > a) memcpy(d + a, h + a, b - a); });
+        }
+        for (auto &x : th) x.join();
+    };
+    size_t prev_o = 0, prev_m = 0;
+    int half = 0;
+    for (size_t o = 0; o < n; o += kHalf, half ^= 1) {
+        const size_t m = std::min(kHalf, n - o);
+        HIPCHK(hipMemcpyAsync(ctx->stage + half * kHalf, src + o, m, hipMemcpyDeviceToHost, s));
+        if (prev_m) fan_out(dst + prev_o, ctx->stage + (half ^ 1) * kHalf, prev_m);   // while the copy runs
+        HIPCHK(hipStreamSynchronize(s));
+        prev_o = o;
+        prev_m = m;
+    }
+    fan_out(dst + prev_o, ctx->stage + (half ^ 1) * kHalf, prev_m);
+    return PPG_OK;
+}
+
+// Pages of [p, p + n) faulted in ahead of a bulk copy into them (huge pages where the kernel
+// allows): a first touch by the copy itself cost ~60 ms per 860 MB of windows (r03)
+void prefault(uint8_t *p, size_t n) {
+    const uintptr_t a = ((uintptr_t)p + 4095) & ~(uintptr_t)4095, z = ((uintptr_t)p + n) & ~(uintptr_t)4095;
+    if (z <= a) return;
+    (void)madvise((void *)a, z - a, MADV_HUGEPAGE);
+#ifdef MADV_POPULATE_WRITE
+    (void)madvise((void *)a, z - a, MADV_POPULATE_WRITE);
+#endif
+}
 
 // capacity for `need` elements, reserved as need x max(scale, 1.5) when it has to grow
 template <class V>
@@ -143,7 +192,11 @@ struct Builder {
     // pass 1
     std::vector<PpgInflateJob> hjobs;
     std::vector<PpgInflateResult> hres;
+    // host block lists, dense: slot q's at hblk[hpos[q]] (a re-run slot's newer list is appended);
+    // addressed by the device's blk_off instead, the 29M-entry array was page-faulted in for a
+    // few entries per piece (r03: 84 ms of zero fill, then 45 ms of faults)
     std::vector<PpgBlockEnd> hblk;
+    std::vector<uint64_t> hpos;
     DevBuf<PpgBlockEnd> blk, bigblk;   // block lists of pass-1 job q at blk_off (bigblk: a piece alone)
     DevBuf<uint8_t> ring;               // 64 Ki 16-bit symbols of output ring per slot
     DevBuf<uint8_t> ident;              // u16 0..32767: the history symbols, for tails of short pieces
@@ -170,10 +223,12 @@ struct Builder {
         HIPCHK(jst.alloc(n));
         HIPCHK(rst.alloc(n));
         HIPCHK(hipMemcpyAsync(jst.p, st.data(), sizeof(PpgInflateJob) * n, hipMemcpyHostToDevice, s));
+        const auto tk = Clock::now();
         HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, jst.p, ident.p, ring.p, rst.p, big ? bigblk.p : blk.p, (int)n));
         std::vector<PpgInflateResult> r(n);
         HIPCHK(hipMemcpyAsync(r.data(), rst.p, sizeof(PpgInflateResult) * n, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        const double t_kern = ms_since(tk);
         for (size_t i = 0; i < n; i++) hres[which[i]] = r[i];
         // the tails: the last 32 Ki symbols (64 KiB) of each ring, gathered as two 32 KiB byte
         // halves; a position before the piece's start is history symbol 32768 + p (ident table)
@@ -206,15 +261,17 @@ struct Builder {
             HIPCHK(dense.alloc(pre.back() + 1));
             HIPCHK(hipMemcpyAsync(dpre.p, pre.data(), 8 * pre.size(), hipMemcpyHostToDevice, s));
             HIPCHK(ppg_launch_pack_blocks(s, blk.p, jst.p, rst.p, dpre.p, dense.p, (int)n));
-            std::vector<PpgBlockEnd> hd(pre.back());
-            if (!hd.empty())
-                HIPCHK(hipMemcpyAsync(hd.data(), dense.p, sizeof(PpgBlockEnd) * hd.size(), hipMemcpyDeviceToHost, s));
+            const size_t h0 = hblk.size();
+            hblk.resize(h0 + pre.back());
+            if (pre.back())
+                HIPCHK(hipMemcpyAsync(hblk.data() + h0, dense.p, sizeof(PpgBlockEnd) * pre.back(), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
-            for (size_t i = 0; i < n; i++)
-                std::copy(hd.begin() + (ptrdiff_t)pre[i], hd.begin() + (ptrdiff_t)pre[i + 1],
-                          hblk.begin() + hjobs[which[i]].blk_off);
+            for (size_t i = 0; i < n; i++) hpos[which[i]] = h0 + pre[i];
         }
         HIPCHK(hipStreamSynchronize(s));
+        if (getenv("PPG_IX_VERBOSE"))
+            fprintf(stderr, "[ix] pass 1 run of %zu jobs: kernel %.1f ms, tails + blocks %.1f\n", n, t_kern,
+                    ms_since(tk) - t_kern);
         return PPG_OK;
     }
     std::vector<PpgBlockEnd> hblk_big;
@@ -223,7 +280,7 @@ struct Builder {
     const PpgBlockEnd *blocks(uint32_t q, uint32_t &nb) const {
         nb = hres[q].nblocks;
         if (!own_blocks[q].empty()) return own_blocks[q].data();
-        return hblk.data() + hjobs[q].blk_off;
+        return hblk.data() + hpos[q];
     }
 };
 
@@ -319,7 +376,8 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     const uint64_t spare_blk = nblk_total;
     nblk_total += (uint64_t)nspare * spare_cap;
     if (nblk_total >= (1ull << 31)) return PPG_UNSUPPORTED;
-    B.hblk.assign(nblk_total, PpgBlockEnd{0, 0});
+    B.hblk.reserve((size_t)(len / 20000) + 4096);   // ~one dynamic block per 30 KB of gzip, grown if more
+    B.hpos.assign(nslots, 0);
     HIPCHK(B.blk.alloc(nblk_total));
     HIPCHK(B.ring.alloc((size_t)nslots * 2 * kRing));
     HIPCHK(B.ta.alloc((size_t)nslots * 2 * kWin));
@@ -329,6 +387,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         HIPCHK(B.ident.alloc(2 * kWin));
         HIPCHK(hipMemcpy(B.ident.p, ident.data(), 2 * kWin, hipMemcpyHostToDevice));
     }
+    if (getenv("PPG_IX_VERBOSE")) fprintf(stderr, "[ix] pass 1 setup %.1f ms\n", ms_since(t));
     {
         std::vector<uint32_t> all(m);
         for (uint32_t q = 0; q < m; q++) all[q] = q;
@@ -490,6 +549,11 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     int64_t records = 0, last_at = -1, last_mark = 0;   // last_mark: output of the last Point or side point
     int batches = 0;
     uint64_t nblocks_seen = 0;
+    static const bool verbose = getenv("PPG_IX_VERBOSE") != nullptr;
+    struct Ev { hipEvent_t e[6] = {}; ~Ev() { for (auto x : e) if (x) (void)hipEventDestroy(x); } } vevs;
+    hipEvent_t *vev = vevs.e;
+    if (verbose)
+        for (int i = 0; i < 6; i++) HIPCHK(hipEventCreate(&vev[i]));
     // CRC-32 of the output (RFC 1952 trailer), raw register R(0, output so far) folded per batch
     static const CrcTables crc_tabs;
     DevBuf<uint32_t> crc_dtab, crc_seg;
@@ -500,6 +564,34 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     ix = ppg_index{};
     std::vector<uint8_t> zeros(kWin, 0);
     ix.add_point(0, hl, 0, 0, zeros.data(), nullptr, 0);   // right after the gzip header (Core.cs:101-102)
+    // The Points' windows land in ix.windows: reserve it for the Point count estimated from the '@'
+    // density of a sample of the resolved histories, and fault its pages in on host threads while
+    // the first batch decodes (r03: ~30 ms per 860 MB of windows when done in line).  A low
+    // estimate only means grow() reallocates later, as without it.
+    struct Joiner {
+        std::vector<std::thread> t;
+        void join() { for (auto &x : t) x.join(); t.clear(); }
+        ~Joiner() { join(); }
+    } prefaulting;
+    {
+        const size_t ns = std::min<size_t>(np, 64);
+        std::vector<uint8_t> smp(ns * kWin);
+        for (size_t i = 0; i < ns; i++)
+            HIPCHK(hipMemcpyAsync(smp.data() + i * kWin, W.p + (1 + i * np / ns) * kWin, kWin, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const size_t ats = (size_t)std::count(smp.begin(), smp.end(), (uint8_t)'@');
+        if (ats && threshold > 0) {
+            const double per_point = (double)threshold * (double)smp.size() / (double)ats;   // output bytes
+            const size_t est = std::min<size_t>((size_t)(1.1 * (double)total / per_point) + 64, total / kWin + 64);
+            ix.windows.reserve(ix.windows.size() + est * kWin);
+            uint8_t *a = ix.windows.data() + ix.windows.size();
+            const size_t n = ix.windows.capacity() - ix.windows.size(), part = (n / 8 + 4095) & ~(size_t)4095;
+            for (int q = 0; q < 8; q++) {
+                const size_t lo = std::min(n, q * part), hi = std::min(n, lo + part);
+                if (hi > lo) prefaulting.t.emplace_back([=] { prefault(a + lo, hi - lo); });
+            }
+        }
+    }
 
     std::vector<PpgInflateJob> h2(np);
     for (size_t j = 0; j < np; j++) {
@@ -511,54 +603,65 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         J.dict_off = (uint64_t)j * kWin;
         J.expect_end = ~0ull;
     }
+    // a second stream for a batch's '@' census (stats kernel), a third for its tails check and CRC,
+    // which follow the census and overlap the host's walk and window copies (r03: census 45 ms +
+    // CRC 49 ms per 100 GB batch, one after the other, before the walk could start)
+    // (declared before the streams: their destructor drains the copies into it)
+    struct Pending {
+        bool on = false;
+        size_t b0 = 0, nbat = 0;
+        uint64_t nb_out = 0;
+        std::vector<uint32_t> hseg, hd;
+    } pend;
+    struct StreamEv {
+        hipStream_t s = nullptr, s3 = nullptr;
+        hipEvent_t e = nullptr, e2 = nullptr;
+        ~StreamEv() {
+            // an early return can leave copies in flight
+            for (hipStream_t x : {s, s3}) if (x) (void)hipStreamSynchronize(x);
+            for (hipEvent_t x : {e, e2}) if (x) (void)hipEventDestroy(x);
+            for (hipStream_t x : {s, s3}) if (x) (void)hipStreamDestroy(x);
+        }
+    } side;
+    HIPCHK(hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&side.e, hipEventDisableTiming));
+    const hipStream_t s2 = side.s;
+    HIPCHK(hipStreamCreateWithFlags(&side.s3, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&side.e2, hipEventDisableTiming));
+    const hipStream_t s3 = side.s3;
+    DevBuf<PpgGather> gat_tails;
+    // a batch's deferred checks, folded in before the next batch overwrites the output
+    auto settle = [&]() -> int {
+        if (!pend.on) return PPG_OK;
+        if (!pend.hseg.empty())
+            HIPCHK(hipMemcpyAsync(pend.hseg.data(), crc_seg.p, 4 * pend.hseg.size(), hipMemcpyDeviceToHost, s3));
+        HIPCHK(hipMemcpyAsync(pend.hd.data(), B.diff.p, 4 * pend.nbat, hipMemcpyDeviceToHost, s3));
+        HIPCHK(hipStreamSynchronize(s3));
+        pend.on = false;
+        if (verbose) {
+            float b = 0;
+            HIPCHK(hipEventElapsedTime(&b, vev[2], vev[3]));
+            fprintf(stderr, "[ix] pass 2 batch: crc %.1f ms (third stream)\n", b);
+        }
+        uint32_t r = 0;   // R(0, batch output) = fold of the segments with Z(., kCrcSeg)
+        for (uint32_t v : pend.hseg) r = crc_tabs.zseg(r) ^ v;
+        crc_raw = (uint32_t)crc32_combine(crc_raw, r, (z_off_t)pend.nb_out);
+        for (size_t i = 0; i < pend.nbat; i++)
+            if (pend.hd[i]) {
+                fprintf(stderr, "ppgpu: GPU CreateIndex: piece %zu does not reproduce its resolved history\n", pend.b0 + i);
+                return PPG_DEVICE_ERROR;
+            }
+        return PPG_OK;
+    };
     size_t b0 = 0;
     while (b0 < np) {
+        if (int rc = settle()) return rc;
         size_t b1 = b0 + 1;
         while (b1 < np && O[b1 + 1] - O[b0] <= cap) b1++;
         const size_t nbat = b1 - b0;
         batches++;
         for (size_t j = b0; j < b1; j++) h2[j].out_off = O[j] - O[b0];
-        HIPCHK(hipMemcpyAsync(jobs2.p + b0, h2.data() + b0, sizeof(PpgInflateJob) * nbat, hipMemcpyHostToDevice, s));
-        HIPCHK(ppg_launch_inflate(s, ctx->ring_bits, ctx->lit_bits, B.comp, B.nwords, jobs2.p + b0, W.p, out.p,
-                                  res2.p + b0, (int)nbat, nullptr));
-        // every piece must hand on exactly the history the next one was resolved to start with
-        std::vector<PpgGather> g(nbat);
-        for (size_t j = b0; j < b1; j++)
-            g[j - b0] = PpgGather{h2[j].out_off, (uint64_t)j * kWin, U[j], ~0ull, (uint64_t)(j + 1) * kWin};
-        HIPCHK(tmp.alloc(nbat * kWin));
-        HIPCHK(B.diff.alloc(nbat));
-        HIPCHK(B.gat.alloc(nbat));
-        HIPCHK(hipMemcpyAsync(B.gat.p, g.data(), sizeof(PpgGather) * nbat, hipMemcpyHostToDevice, s));
-        HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, tmp.p, W.p, B.diff.p, (int)nbat));
-        // CRC-32 of the batch's output: front-padded to whole kCrcSeg segments, one wave each
-        const uint64_t nb_out = O[b1] - O[b0];
-        const uint64_t crc_pad = (kCrcSeg - nb_out % kCrcSeg) % kCrcSeg;
-        const uint64_t nseg = (nb_out + crc_pad) / kCrcSeg;
-        HIPCHK(crc_seg.alloc(std::max<uint64_t>(nseg, 1)));
-        HIPCHK(ppg_launch_crc(s, out.p, nb_out, crc_pad, crc_dtab.p, crc_seg.p, nseg));
-        std::vector<uint32_t> hseg(nseg);
-        if (nseg) HIPCHK(hipMemcpyAsync(hseg.data(), crc_seg.p, 4 * nseg, hipMemcpyDeviceToHost, s));
-        std::vector<PpgInflateResult> r2(nbat);
-        std::vector<uint32_t> hd(nbat);
-        HIPCHK(hipMemcpyAsync(r2.data(), res2.p + b0, sizeof(PpgInflateResult) * nbat, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(hd.data(), B.diff.p, 4 * nbat, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        {
-            uint32_t r = 0;   // R(0, batch output) = fold of the segments with Z(., kCrcSeg)
-            for (uint32_t v : hseg) r = crc_tabs.zseg(r) ^ v;
-            crc_raw = (uint32_t)crc32_combine(crc_raw, r, (z_off_t)nb_out);
-        }
-        for (size_t i = 0; i < nbat; i++) {
-            if (r2[i].status != PPG_OK) return r2[i].status;
-            if (r2[i].produced != U[b0 + i]) return PPG_DATA_ERROR;
-            if (hd[i]) {
-                fprintf(stderr, "ppgpu: GPU CreateIndex: piece %zu does not reproduce its resolved history\n", b0 + i);
-                return PPG_DEVICE_ERROR;
-            }
-        }
-
-        // ---- 4. '@' census of the batch's blocks and the Points among them ----
-        const auto tc = Clock::now();
+        // the batch's blocks as output spans (pass 1's block lists), uploaded ahead of the decode
         std::vector<PpgSpan> hs;
         struct BlockRef { uint32_t j; uint64_t end_bit, rel_end; };
         std::vector<BlockRef> refs;
@@ -577,10 +680,70 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             HIPCHK(spans.alloc(hs.size()));
             HIPCHK(dstats.alloc(hs.size()));
             HIPCHK(hipMemcpyAsync(spans.p, hs.data(), sizeof(PpgSpan) * hs.size(), hipMemcpyHostToDevice, s));
-            HIPCHK(ppg_launch_at_stats(s, out.p, spans.p, dstats.p, (int)hs.size()));
-            HIPCHK(hipMemcpyAsync(st.data(), dstats.p, sizeof(PpgAtStats) * hs.size(), hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
         }
+        HIPCHK(hipMemcpyAsync(jobs2.p + b0, h2.data() + b0, sizeof(PpgInflateJob) * nbat, hipMemcpyHostToDevice, s));
+        if (verbose) HIPCHK(hipEventRecord(vev[0], s));
+        HIPCHK(ppg_launch_inflate(s, ctx->ring_bits, ctx->lit_bits, B.comp, B.nwords, jobs2.p + b0, W.p, out.p,
+                                  res2.p + b0, (int)nbat, nullptr));
+        if (verbose) HIPCHK(hipEventRecord(vev[1], s));
+        HIPCHK(hipEventRecord(side.e, s));
+        const auto tb = Clock::now();
+        if (!hs.empty()) {   // ---- 4. '@' census of the batch's blocks (second stream) ----
+            HIPCHK(hipStreamWaitEvent(s2, side.e, 0));
+            if (verbose) HIPCHK(hipEventRecord(vev[4], s2));
+            HIPCHK(ppg_launch_at_stats(s2, out.p, spans.p, dstats.p, (int)hs.size()));
+            if (verbose) HIPCHK(hipEventRecord(vev[5], s2));
+            HIPCHK(hipMemcpyAsync(st.data(), dstats.p, sizeof(PpgAtStats) * hs.size(), hipMemcpyDeviceToHost, s2));
+            HIPCHK(hipEventRecord(side.e2, s2));
+        }
+        // third stream, checked later (settle): every piece must hand on exactly the history the
+        // next one was resolved to start with, and the CRC-32 of the batch's output (front-padded
+        // to whole kCrcSeg segments, one wave each) -- they overlap the host's walk and windows
+        {
+            std::vector<PpgGather> g(nbat);
+            for (size_t j = b0; j < b1; j++)
+                g[j - b0] = PpgGather{h2[j].out_off, (uint64_t)j * kWin, U[j], ~0ull, (uint64_t)(j + 1) * kWin};
+            HIPCHK(tmp.alloc(nbat * kWin));
+            HIPCHK(B.diff.alloc(nbat));
+            HIPCHK(gat_tails.alloc(nbat));
+            HIPCHK(hipMemcpyAsync(gat_tails.p, g.data(), sizeof(PpgGather) * nbat, hipMemcpyHostToDevice, s3));
+            // after the census, which the host's walk waits for; these overlap that walk
+            HIPCHK(hipStreamWaitEvent(s3, hs.empty() ? side.e : side.e2, 0));
+            HIPCHK(ppg_launch_gather(s3, out.p, W.p, gat_tails.p, tmp.p, W.p, B.diff.p, (int)nbat));
+            pend.nb_out = O[b1] - O[b0];
+            const uint64_t crc_pad = (kCrcSeg - pend.nb_out % kCrcSeg) % kCrcSeg;
+            const uint64_t nseg = (pend.nb_out + crc_pad) / kCrcSeg;
+            HIPCHK(crc_seg.alloc(std::max<uint64_t>(nseg, 1)));
+            if (verbose) HIPCHK(hipEventRecord(vev[2], s3));
+            HIPCHK(ppg_launch_crc(s3, out.p, pend.nb_out, crc_pad, crc_dtab.p, crc_seg.p, nseg));
+            if (verbose) HIPCHK(hipEventRecord(vev[3], s3));
+            // (read back in settle: a copy into pageable memory holds the host until it has run)
+            pend.hseg.assign(nseg, 0);
+            pend.hd.assign(nbat, 0);
+            pend.b0 = b0;
+            pend.nbat = nbat;
+            pend.on = true;
+        }
+        std::vector<PpgInflateResult> r2(nbat);
+        HIPCHK(hipMemcpyAsync(r2.data(), res2.p + b0, sizeof(PpgInflateResult) * nbat, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipStreamSynchronize(s2));   // (before any return: its copy lands in st)
+        for (size_t i = 0; i < nbat; i++) {
+            if (r2[i].status != PPG_OK) return r2[i].status;
+            if (r2[i].produced != U[b0 + i]) return PPG_DATA_ERROR;
+        }
+        if (verbose) {
+            float a = 0, c = 0, d = 0;
+            HIPCHK(hipEventElapsedTime(&a, vev[0], vev[1]));
+            HIPCHK(hipEventElapsedTime(&c, vev[4], vev[5]));
+            HIPCHK(hipEventElapsedTime(&d, vev[1], vev[5]));
+            fprintf(stderr, "[ix] pass 2 batch %d: inflate %.1f ms, census kernel %.1f (ends %.1f after the inflate); "
+                            "census on the host %.1f ms after launch\n", batches, a, c, d, ms_since(tb));
+        }
+
+        // ---- 4. the Points among the batch's blocks (Core.cs:79-110) ----
+        const auto tc = Clock::now();
+        const double t_stats = 0;   // (the census ran on the second stream, beside the CRC)
         const bool final_batch = b1 == np;
         struct Pick { int64_t bits, input, output; uint32_t j; uint64_t rel; int64_t off_len; };
         std::vector<Pick> picks;
@@ -623,6 +786,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
             }
         }
         nblocks_seen += refs.size();
+        const double t_walk = ms_since(tc);
         // windows of the picked Points, then the side points', gathered on the device in index order
         // and copied straight onto the index's window arrays (a zero-output Point reads W[0]: zeros)
         std::vector<PpgGather> gw;
@@ -633,6 +797,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         // grown to the whole member's projected size (at least x1.5): an exact per-batch reserve
         // recopied every window so far on every batch (quadratic in the batch count)
         const double proj = 1.02 * (double)total / (double)std::max<uint64_t>(O[b1], 1);
+        prefaulting.join();   // (before grow() may move the array)
         grow(ix.pts, ix.pts.size() + picks.size(), proj);
         grow(ix.windows, ix.windows.size() + picks.size() * kWin, proj);
         grow(ix.side_bit, ix.side_bit.size() + sides.size(), proj);
@@ -641,17 +806,31 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         const size_t w0 = ix.windows.size(), s0 = ix.side_win.size();
         ix.windows.resize(w0 + picks.size() * kWin);          // uninitialised (ByteVec)
         ix.side_win.resize(s0 + sides.size() * kWin);
+        const auto tw = Clock::now();
+        {   // fault the new window pages in from 8 threads (huge pages where allowed)
+            std::thread th[8];
+            const size_t nw = picks.size() * kWin, part = (nw / 8 + 4095) & ~(size_t)4095;
+            for (int q = 0; q < 8; q++) {
+                const size_t a = std::min(nw, q * part), z = std::min(nw, a + part);
+                th[q] = std::thread([&, a, z] { if (z > a) prefault(ix.windows.data() + w0 + a, z - a); });
+            }
+            for (auto &x : th) x.join();
+        }
+        const double t_fault = ms_since(tw);
+        double t_alloc = 0, t_gat = 0;
         if (!gw.empty()) {
             HIPCHK(B.gat.alloc(gw.size()));
             HIPCHK(dwin.alloc(gw.size() * kWin));
+            t_alloc = ms_since(tw) - t_fault;
             HIPCHK(hipMemcpyAsync(B.gat.p, gw.data(), sizeof(PpgGather) * gw.size(), hipMemcpyHostToDevice, s));
             HIPCHK(ppg_launch_gather(s, out.p, W.p, B.gat.p, dwin.p, nullptr, nullptr, (int)gw.size()));
-            if (!picks.empty())
-                HIPCHK(hipMemcpyAsync(ix.windows.data() + w0, dwin.p, picks.size() * kWin, hipMemcpyDeviceToHost, s));
-            if (!sides.empty())
-                HIPCHK(hipMemcpyAsync(ix.side_win.data() + s0, dwin.p + picks.size() * kWin, sides.size() * kWin,
-                                      hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
+            if (verbose) {
+                HIPCHK(hipStreamSynchronize(s));
+                t_gat = ms_since(tw) - t_fault - t_alloc;
+            }
+            if (int rc = copy_d2h_staged(ctx, s, ix.windows.data() + w0, dwin.p, picks.size() * kWin)) return rc;
+            if (int rc = copy_d2h_staged(ctx, s, ix.side_win.data() + s0, dwin.p + picks.size() * kWin, sides.size() * kWin))
+                return rc;
         }
         for (const Side &d : sides) {
             ix.side_bit.push_back((int64_t)d.end_bit);
@@ -666,8 +845,15 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
                 ix.add_point_fields((int)p.bits, p.input, p.output, w + kWin - p.off_len, (size_t)p.off_len);
         }
         t_census += ms_since(tc);
+        if (verbose)
+            fprintf(stderr, "[ix] batch %d: %zu pieces, %zu blocks, census: stats %.1f ms, walk %.1f, windows %.1f (%zu; "
+                            "grow %.1f, prefault %.1f, alloc %.1f, gather %.1f, copy + points %.1f)\n",
+                    batches, nbat, hs.size(), t_stats, t_walk - t_stats, ms_since(tc) - t_walk, gw.size(),
+                    std::chrono::duration<double, std::milli>(tw - tc).count() - t_walk, t_fault, t_alloc, t_gat,
+                    ms_since(tw) - t_fault - t_alloc - t_gat);
         b0 = b1;
     }
+    if (int rc = settle()) return rc;
     stat[3] = ms_since(t) - t_census;
     stat[4] = t_census;
     stat[10] = (double)batches;

@@ -95,6 +95,14 @@ struct __attribute__((aligned(16))) InflateLds {
     uint32_t cen[8];               // newline census: count, previous byte was '\n', PPG_PF_* flags, cap, shift, dst
 };
 
+#ifdef PPG_IX_STATS
+// diagnostic build only (EXTRA=-DPPG_IX_STATS): CreateIndex pass 1's history-symbol output -- how
+// many output bytes are copies of the piece's unknown starting history, and how far into the piece
+// the last one lies ([0] symbols, [1] sum of last positions + 1, [2] bytes, [3] jobs, [4..13] jobs
+// by last position / bytes in tenths, [14] the largest last position)
+__device__ unsigned long long ppg_ixstat[16];
+#endif
+
 #ifdef PPG_STAMPS
 // diagnostic build only (EXTRA=-DPPG_STAMPS): s_memtime stamps at the phase boundaries of every
 // token round, summed per wave and added to these totals at the end of each chunk; the launcher
@@ -661,8 +669,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     int status = ST_OK, flags = 0, last = 0, in_block = 0;
     Canon clit = {0, 0, 0}, cdst = {0, 0, 0};   // per-lane canonical codes of the current block
     // flush of chunk positions [lo, hi) (never across a UNIT boundary except the plain case)
+#ifdef PPG_IX_STATS
+    uint64_t ix_unk = 0;
+    uint32_t ix_last = 0;
+#endif
     auto flush = [&](uint32_t lo, uint32_t hi) {
         if constexpr (IX) {
+#ifdef PPG_IX_STATS
+            for (uint32_t p0 = lo; p0 < hi; p0 += 64) {
+                const uint32_t p = p0 + (uint32_t)lane;
+                const uint64_t b = __ballot(p < hi && S.ring[(rb0 + p) & RM] < 0x8000u);
+                ix_unk += (uint64_t)__popcll(b);
+                if (b) ix_last = p0 + 64u - (uint32_t)__clzll(b);
+            }
+#endif
             const uint64_t g = out_off + (lo & IX_RING_MASK);
             flush_range_sym<RB>(S.ring, (uint16_t *)out, g, g + (hi - lo), lane);
         } else {
@@ -1172,6 +1192,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                "bitserial lit %u eob %u match %u\n", k, pos, st_rounds, st_tokens, st_spec, st_short, st_far, st_dep,
                st_dbl, st_blit, st_beob, st_bmatch);
 #endif
+#ifdef PPG_IX_STATS
+    if (IX && lane == 0) {
+        atomicAdd(&ppg_ixstat[0], (unsigned long long)ix_unk);
+        atomicAdd(&ppg_ixstat[1], (unsigned long long)ix_last);
+        atomicAdd(&ppg_ixstat[2], (unsigned long long)pos);
+        atomicAdd(&ppg_ixstat[3], 1ull);
+        atomicAdd(&ppg_ixstat[4 + min(9u, (uint32_t)(10ull * ix_last / max(pos, 1u)))], 1ull);
+        atomicMax(&ppg_ixstat[14], (unsigned long long)ix_last);
+    }
+#endif
 #ifdef PPG_STAMPS
     if (!IX && lane == 0) {
         atomicAdd(&ppg_stamp_acc[0], (unsigned long long)sa_dec);
@@ -1266,6 +1296,19 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
     hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64),
                        sizeof(InflateLds<10, 8, uint16_t>), s, comp,
                        nwords, jobs, dicts, out, res, njobs, blk, nullptr);
+#ifdef PPG_IX_STATS
+    {
+        unsigned long long h[16] = {0};
+        if (hipStreamSynchronize(s) == hipSuccess && hipMemcpyFromSymbol(h, HIP_SYMBOL(ppg_ixstat), sizeof h) == hipSuccess) {
+            const unsigned long long z[16] = {0};
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(ppg_ixstat), z, sizeof z);
+            fprintf(stderr, "PPG_IX_STATS jobs %llu bytes %llu unknown %llu (%.4f%%) mean last %.0f max last %llu tenths", h[3],
+                    h[2], h[0], 100.0 * h[0] / (h[2] ? h[2] : 1), (double)h[1] / (h[3] ? h[3] : 1), h[14]);
+            for (int i = 4; i < 14; i++) fprintf(stderr, " %llu", h[i]);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
     return hipGetLastError();
 }
 
