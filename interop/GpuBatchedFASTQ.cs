@@ -8,7 +8,8 @@
 //    into one managed array that the batch's FastqRecords slice (a record stays valid after the
 //    next MoveNext here; the reference invalidates it, Q9);
 //  * Count(): ppg_file_decompress_all on one GPU, or ppg_dist_decompress_all when the process is
-//    one rank of a multi-GPU job (GpuJob: the ranks' RCCL communicator).
+//    one rank of a multi-GPU job (GpuJob: the ranks' RCCL communicator);
+//  * a rank of a multi-GPU job enumerates its own share (ppg_partition's chunk range).
 // (Source only: no .NET SDK in this image; tests/test_interop_cs.py checks the externs it uses.)
 using System;
 using System.Collections;
@@ -64,7 +65,9 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
         _OwnCtx = true;
     }
 
-    /// <summary>This process is one rank of a multi-GPU job: Count() decodes the rank's share.</summary>
+    /// <summary>This process is one rank of a multi-GPU job: Count() decodes the rank's share and
+    /// gathers every rank's counts; enumeration yields this rank's share of the records (the chunk
+    /// range ppg_partition gives it), so the ranks' records in rank order are the file's.</summary>
     public GpuBatchedFASTQ(string indexPath, string gzipPath, GpuJob job)
     {
         PpGpu.Check(PpGpu.ppg_index_deserialize(indexPath, out _Ix));
@@ -80,7 +83,7 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
     private readonly int _Threads;
     private readonly GpuJob? _Job;
 
-    /// <summary>Text per streamed batch (ppg_cursor keeps three batches in flight in pinned host
+    /// <summary>Text per streamed batch (ppg_cursor keeps four batches in flight in pinned host
     /// memory).  Any size: each chunk is copied into its own managed array (a chunk is below 2^31
     /// bytes, ppg_index_validate), so a batch may exceed a managed array's limit.</summary>
     public long BatchBytes
@@ -107,8 +110,8 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
     // an iterator may not contain unsafe code: the batch is read by NextBatch, the records yielded here
     public IEnumerator<FastqRecord> GetEnumerator()
     {
-        int chunks = PpGpu.ppg_index_count(_Ix) - 1;
-        PpGpu.Check(PpGpu.ppg_cursor_open(_Ctx, _Ix, _Path, 0, chunks, BatchBytes, _Threads, out var cur));
+        var (first, n) = ChunkRange();
+        PpGpu.Check(PpGpu.ppg_cursor_open(_Ctx, _Ix, _Path, first, n, BatchBytes, _Threads, out var cur));
         try
         {
             while (true)
@@ -122,6 +125,16 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
         {
             PpGpu.ppg_cursor_close(cur);
         }
+    }
+
+    // The chunks this enumerator streams: all of them, or (multi-GPU job) this rank's share
+    private unsafe (int first, int n) ChunkRange()
+    {
+        int chunks = PpGpu.ppg_index_count(_Ix) - 1;
+        if (_Job == null) return (0, chunks);
+        var bounds = new int[_Job.NRanks + 1];
+        fixed (int* b = bounds) PpGpu.Check(PpGpu.ppg_partition(_Ix, 0, chunks, _Job.NRanks, b));
+        return (bounds[_Job.Rank], bounds[_Job.Rank + 1] - bounds[_Job.Rank]);
     }
 
     // The next batch's records, or null after the last batch.  Each chunk's raw bytes are copied

@@ -677,7 +677,7 @@ class BatchedFASTQ:
     canonical order: chunk 0's records, then chunk 1's, ...  enable_ssd_optimization is accepted
     for signature parity (it selected 1 or 8 FileStreams, LazyFileReader.cs:27-33)."""
 
-    def __init__(self, index, gzip_path, enable_ssd_optimization=False, device=None):
+    def __init__(self, index, gzip_path, enable_ssd_optimization=False, device=None, rank=None, world=None):
         if isinstance(index, (str, os.PathLike)):
             index = IndexIO.Deserialize(index)
         self.index = index
@@ -685,6 +685,20 @@ class BatchedFASTQ:
         self.enable_ssd_optimization = enable_ssd_optimization
         self.dev = device
         self._shard = None
+        # one rank of a multi-GPU job (the reference's Task.Run fan-out, BatchedFASTQ.cs:62-77, on
+        # GPUs): iteration yields this rank's share -- the contiguous chunk range ppg_partition
+        # gives it -- so the ranks' records, concatenated in rank order, are the file's
+        self.rank, self.world = rank, world
+        if (rank is None) != (world is None) or (world is not None and not 0 <= rank < world):
+            raise ValueError("rank and world go together, 0 <= rank < world")
+
+    def chunk_range(self):
+        """(first, n): the chunks this enumerator streams (all of them, or this rank's share)."""
+        m = self.index.Count - 1
+        if self.world is None:
+            return 0, m
+        b = partition(self.index, self.world, 0, m)
+        return int(b[self.rank]), int(b[self.rank + 1] - b[self.rank])
 
     def _run(self):
         if self._shard is None:
@@ -711,7 +725,8 @@ class BatchedFASTQ:
     def __iter__(self):
         """Records streamed through ppg_cursor in bounded memory, canonical chunk order; each
         batch's bytes are copied out before the next one is requested."""
-        cur = Cursor(self.index, self.gzip_path, batch_bytes=self.batch_bytes,
+        first, n = self.chunk_range()
+        cur = Cursor(self.index, self.gzip_path, first=first, n=n, batch_bytes=self.batch_bytes,
                      threads=16 if self.enable_ssd_optimization else 8, device=self.dev)
         try:
             for b in cur:

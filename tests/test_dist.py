@@ -6,6 +6,7 @@ import socket
 import numpy as np
 import pytest
 
+import parallelparsing_amd as pp
 from conftest import load_case
 from parallelparsing_amd.dist import partition_chunks
 
@@ -174,3 +175,20 @@ def test_host_comm_refuses_a_stale_segment():
         pr.join(30)
     finally:
         os.remove(path)
+
+
+@pytest.mark.parametrize("world", [1, 2, 5])
+def test_rank_enumerators_cover_the_file_in_order(world):
+    """BatchedFASTQ(rank=, world=): each rank streams its ppg_partition share; the shares are
+    contiguous, in rank order and cover every chunk (the multi-GPU enumeration surface)."""
+    meta, gz = load_case("l6_c200")
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    m = ix.Count - 1
+    nxt = 0
+    for r in range(world):
+        first, n = pp.BatchedFASTQ(ix, "unused.gz", rank=r, world=world).chunk_range()
+        assert first == nxt and n >= 0
+        nxt = first + n
+    assert nxt == m
+    with pytest.raises(ValueError):
+        pp.BatchedFASTQ(ix, "unused.gz", rank=world, world=world)

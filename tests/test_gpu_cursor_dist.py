@@ -83,6 +83,28 @@ def test_cursor_large_file_records_equal_oracle(tmp_path, device):
     assert recs[0].identifier == txt[1:txt.tobytes().index(b"\n")].tobytes()
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank_enumeration_concatenates_to_the_file(world, tmp_path, device):
+    """Multi-GPU enumeration (VERDICT r02 missing #5): each rank's BatchedFASTQ yields the records
+    of its ppg_partition share; in rank order they are exactly the single-GPU enumeration's."""
+    meta, gz = load_case("l6_c200")
+    p = tmp_path / "f.gz"
+    p.write_bytes(gz)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    whole = pp.BatchedFASTQ(ix, str(p), device=device)
+    whole.batch_bytes = 1 << 16
+    exp = [(r.identifier, r.sequence, r.other, r.quality) for r in whole]
+    got, ranges = [], []
+    for r in range(world):
+        bf = pp.BatchedFASTQ(ix, str(p), device=device, rank=r, world=world)
+        bf.batch_bytes = 1 << 16
+        ranges.append(bf.chunk_range())
+        got += [(x.identifier, x.sequence, x.other, x.quality) for x in bf]
+    assert all(n > 0 for _, n in ranges) and ranges[0][0] == 0
+    assert all(ranges[i][0] + ranges[i][1] == ranges[i + 1][0] for i in range(world - 1))
+    assert got == exp and len(got) == meta["total_records"]
+
+
 def test_rccl_comm_world1(device):
     meta, gz = load_case("l6_c200")
     ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
