@@ -49,6 +49,30 @@ def test_cursor_batches_match_golden(name, tmp_path, device):
     assert k == n and base == meta["total_records"]
 
 
+@pytest.mark.parametrize("pack,slots", [("0", "2"), ("1", "5"), ("2", "3")])
+def test_cursor_transfer_modes_match_golden(pack, slots, tmp_path, device, monkeypatch):
+    """Every way a batch can reach the host (PPG_CURSOR_PACK: per-chunk copies, device pack + one
+    copy, pack kernel storing into pinned memory) and slot counts give the golden bytes/records."""
+    monkeypatch.setenv("PPG_CURSOR_PACK", pack)
+    monkeypatch.setenv("PPG_CURSOR_SLOTS", slots)
+    meta, gz = load_case("l6_c20")
+    p = tmp_path / "f.gz"
+    p.write_bytes(gz)
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    n = ix.Count - 1
+    cur = pp.Cursor(ix, str(p), batch_bytes=max(1, int(ix.point_fields(n)[0]) // 7), threads=2, device=device)
+    assert cur.batches > int(slots)
+    k = 0
+    for b in cur:
+        for j in range(b.nchunks):
+            c = meta["chunks"][k]
+            raw = b.raw(j)
+            assert sha(raw[len(ix[k].offset):]) == c["sha256"], (pack, k)
+            assert sha(np.ascontiguousarray(b.records(j), "<u4").tobytes()) == c["rec_sha256"], (pack, k)
+            k += 1
+    assert k == n
+
+
 def test_cursor_large_file_records_equal_oracle(tmp_path, device):
     """200k records through ~8 MB batches (>40 of them), every record's fields vs the oracle."""
     import ctypes as C
