@@ -13,9 +13,13 @@
 // Root-table entries (the lane-parallel decoder's format).  Every field is placed so that one
 // VALU op extracts or applies it: bits [4:0] are the code length (bit 4 always 0), so
 // v_alignbit / v_lshrrev consume the code straight from the entry.
-//  litlen: [3:0] code length L, 0 = decode bit-serially (end-of-block, invalid symbol, or a code
-//          longer than the root table), [9:5] L + length extra bits, [14:10] length extra bits,
-//          [15] length symbol, [31:16] literal byte or length base
+//  litlen: a literal's entry is its finished token word (the decoder's format: [7:0] bits = L,
+//          [16:8] bytes = 1, [31:17] 0x100 | byte), and an entry to decode bit-serially (end-of-
+//          block, invalid symbol, or a code longer than the root table) the special token word
+//          (bits 128, bytes 0, field 0x100); both have bit 15 clear.  A length symbol's entry:
+//          [3:0] code length L, [9:5] L + length extra bits, [14:10] length extra bits, [15] set,
+//          [31:16] length base.  (r03: the decoder selects a literal's word instead of assembling
+//          it from fields, ~10 VALU fewer per candidate.)
 //  dist:   [3:0] L2 (0 = bit-serial), [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base
 //  code-length code: [3:0] L, [15:8] symbol
 
@@ -29,6 +33,10 @@ __constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 1
 
 enum { TAB_LIT = 0, TAB_DST = 1, TAB_CL = 2 };
 
+// the decoder's token word of a token its root tables cannot resolve: 128 bits (ends the walk),
+// 0 bytes, field 0x100
+#define PPG_SPECIAL_TOKEN (128u | (0x100u << 17))
+
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
@@ -41,8 +49,8 @@ __device__ __forceinline__ uint32_t rdlane_u(uint32_t v, uint32_t l) {
 __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int kind) {
     if (kind == TAB_CL) return len | (sym << 8);
     if (kind == TAB_LIT) {
-        if (sym < 256) return len | (len << 5) | (sym << 16);
-        if (sym == 256 || sym >= 286) return 0u;
+        if (sym < 256) return len | (1u << 8) | ((0x100u | sym) << 17);
+        if (sym == 256 || sym >= 286) return PPG_SPECIAL_TOKEN;
         const uint32_t x = c_lext[sym - 257];
         return len | ((len + x) << 5) | (x << 10) | 0x8000u | ((uint32_t)c_lbase[sym - 257] << 16);
     }
@@ -52,7 +60,8 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int k
 }
 
 // Builds a canonical-Huffman root table of 2^TB entries from n code lengths (all 64 lanes).
-// Codes longer than TB (and unused patterns of an incomplete code) get entry 0 -> bit-serial path,
+// Codes longer than TB (and unused patterns of an incomplete code) get the bit-serial entry (0, or
+// the special token word in a litlen table) -> bit-serial path,
 // which decodes bit-by-bit from count[]/sorted[].  Validity follows zlib 1.2.11 inflate_table:
 // over-subscribed -> error; incomplete -> error unless exactly one code of length 1 (not for
 // the code-length code); no codes at all -> accepted (decoding then fails).  Returns 0 / -1.
@@ -115,7 +124,8 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, Canon *c
     __syncthreads();
     for (int e0 = 0; e0 < (1 << TB); e0 += 64) {   // uniform trip count (see ppg_inflate_kernel)
         const int e = e0 + lane;
-        uint32_t code = 0, first = 0, index = 0, entry = 0;
+        // not found (longer than TB, or an unused pattern of an incomplete code): bit-serial
+        uint32_t code = 0, first = 0, index = 0, entry = kind == TAB_LIT ? PPG_SPECIAL_TOKEN : 0u;
         bool found = false;
 #pragma unroll 1
         for (int l = 1; l <= TB; l++) {

@@ -490,6 +490,8 @@ __device__ __forceinline__ void copy_match(RingT *ring, const uint8_t *ob, uint3
 template <int LBT>
 __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32_t *dst, uint32_t lo, uint32_t hi,
                                                uint32_t lane) {
+    // a literal's (or a special code's) root entry is already its token word; only a length
+    // symbol's entry (bit 15) is assembled from the two tables (ppg_huffman.h, r03)
     const uint32_t e = lit[lo & ((1u << LBT) - 1)];
     const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
     const uint32_t xb = (e >> 10) & 31;
@@ -499,16 +501,14 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     const uint32_t r2 = y >> (d & 31);                              // past the distance code
     const uint32_t xd = (d >> 10) & 31;
     const uint32_t dist = (d >> 16) + (r2 & ((1u << xd) - 1));
-    const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);       // length symbol: all ones
-    const uint32_t tb = ((e >> 5) & 31) + (((d >> 5) & 31) & lm);
-    const uint32_t nb = ((mlen - 1) & lm) + 1;                      // output bytes
-    // special: all ones (one v_min + v_cmp: no SALU mask arithmetic)
-    const uint32_t sm = min(e & 15u, (d & 15u) | ~lm) == 0u ? ~0u : 0u;
-    const uint32_t field = ((dist - 1) & lm) | ((0x100u | (e >> 16)) & ~lm);
-    const uint32_t tok = tb | (nb << 8) | (field << 17);
-    return (tok & ~sm) | ((128u | (0x100u << 17)) & sm);
+    const uint32_t tb = ((e >> 5) & 31) + ((d >> 5) & 31);
+    const uint32_t tlen = tb | (mlen << 8) | ((dist - 1) << 17);
+    // selects as bit masks (a ?: became a divergent branch: exec juggling costs more than the VALU)
+    const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);               // length symbol: all ones
+    const uint32_t sd = (uint32_t)((int32_t)((d & 15u) - 1u) >> 31);        // bit-serial distance: all ones
+    const uint32_t t2 = (tlen & ~sd) | (PPG_SPECIAL_TOKEN & sd);
+    return (t2 & lm) | (e & ~lm);
 }
-
 // The walk loop of the decoder (see Round): per token v_readlane (candidate X[5:0]),
 // v_writelane (at output offset (X >> 8)[5:0]), one s_add, and s_and's SCC as the loop test —
 // written out because the compiler adds an s_cmp_eq 0 after the s_and (one more SALU per token,
