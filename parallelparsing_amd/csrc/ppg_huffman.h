@@ -20,7 +20,8 @@
 //          [3:0] code length L, [9:5] L + length extra bits, [14:10] length extra bits, [15] set,
 //          [31:16] length base.  (r03: the decoder selects a literal's word instead of assembling
 //          it from fields, ~10 VALU fewer per candidate.)
-//  dist:   [3:0] L2 (0 = bit-serial), [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base
+//  dist:   [3:0] L2 (0 = bit-serial), [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base - 1
+//          (the token word's field is distance - 1)
 //  code-length code: [3:0] L, [15:8] symbol
 
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -56,7 +57,7 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int k
     }
     if (sym >= 30) return 0u;
     const uint32_t x = c_dext[sym];
-    return len | ((len + x) << 5) | (x << 10) | ((uint32_t)c_dbase[sym] << 16);
+    return len | ((len + x) << 5) | (x << 10) | ((uint32_t)(c_dbase[sym] - 1) << 16);
 }
 
 // Builds a canonical-Huffman root table of 2^TB entries from n code lengths (all 64 lanes).

@@ -494,20 +494,23 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     // symbol's entry (bit 15) is assembled from the two tables (ppg_huffman.h, r03)
     const uint32_t e = lit[lo & ((1u << LBT) - 1)];
     const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
-    const uint32_t xb = (e >> 10) & 31;
-    const uint32_t mlen = (e >> 16) + (r1 & ((1u << xb) - 1));
-    const uint32_t y = r1 >> xb;
-    const uint32_t d = dst[y & ((1u << DB) - 1)];
-    const uint32_t r2 = y >> (d & 31);                              // past the distance code
-    const uint32_t xd = (d >> 10) & 31;
-    const uint32_t dist = (d >> 16) + (r2 & ((1u << xd) - 1));
+    // xs[4:0] = the length's extra bits: shift / bit-field operands use only their low 5 bits
+    const uint32_t xs = e >> 10;
+    const uint32_t mlen = (e >> 16) + __builtin_amdgcn_ubfe(r1, 0u, xs);
+    const uint32_t y = __builtin_amdgcn_alignbit(0u, r1, xs);      // past the extra bits
+    const uint32_t d = dst[__builtin_amdgcn_ubfe(r1, xs, (uint32_t)DB)];
+    // distance - 1 = (base - 1) + the extra bits after the distance code (d[4:0] = L2, (d >> 10)[4:0] = extra)
+    const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(y, d, d >> 10);
     const uint32_t tb = ((e >> 5) & 31) + ((d >> 5) & 31);
-    const uint32_t tlen = tb | (mlen << 8) | ((dist - 1) << 17);
-    // selects as bit masks (a ?: became a divergent branch: exec juggling costs more than the VALU)
-    const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);               // length symbol: all ones
-    const uint32_t sd = (uint32_t)((int32_t)((d & 15u) - 1u) >> 31);        // bit-serial distance: all ones
-    const uint32_t t2 = (tlen & ~sd) | (PPG_SPECIAL_TOKEN & sd);
-    return (t2 & lm) | (e & ~lm);
+    const uint32_t tlen = tb | (mlen << 8) | (dm1 << 17);
+    const uint32_t t2 = (d & 15u) ? tlen : PPG_SPECIAL_TOKEN;             // bit-serial distance code
+    // e for a literal / special entry, t2 for a length symbol's (bit 15): one v_bfi on the sign-
+    // extended flag (a ?: here became a divergent branch -- exec juggling costs more than the VALU --
+    // or, written as masks, three instructions)
+    const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);
+    uint32_t tok;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tok) : "v"(lm), "v"(t2), "v"(e));
+    return tok;
 }
 // The walk loop of the decoder (see Round): per token v_readlane (candidate X[5:0]),
 // v_writelane (at output offset (X >> 8)[5:0]), one s_add, and s_and's SCC as the loop test —
