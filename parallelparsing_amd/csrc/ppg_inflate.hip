@@ -610,9 +610,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
     // adds at most 64 + 258 bytes, so UNIT <= RING - 386 keeps them flushed (see copy_match)
     constexpr uint32_t UNIT = RB >= 13 ? 4096u : RING / 2;
     static_assert(RB >= 10 && RB <= 15, "ring of 1..32 KiB");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using RingT = typename std::conditional<IX, uint16_t, uint8_t>::type;   // IX: 16-bit symbols
-    InflateLds<RB, LBT, RingT> &S = *reinterpret_cast<InflateLds<RB, LBT, RingT> *>(smem);
+    // static LDS: every address is a link-time constant the compiler folds into the instructions'
+    // offsets (a dynamic extern array cost one v_add of its base per ring access, r03)
+    __shared__ InflateLds<RB, LBT, RingT> S;
     const int lane = threadIdx.x;
     const int k = blockIdx.x;
     if (k >= njobs) return;
@@ -1262,10 +1263,10 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
     if (ring_bits == R && lit_bits == L) {                                                                    \
         if (nls)                                                                                              \
             hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, true>), dim3(njobs), dim3(64),                \
-                               sizeof(InflateLds<R, L>), s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls); \
+                               0, s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls);                 \
         else                                                                                                  \
             hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, false>), dim3(njobs), dim3(64),               \
-                               sizeof(InflateLds<R, L>), s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls); \
+                               0, s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls);                 \
         PPG_STAMP_DUMP(s);                                                                                    \
         return hipGetLastError();                                                                             \
     }
@@ -1296,8 +1297,7 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs) {
     if (njobs <= 0) return hipSuccess;
-    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64),
-                       sizeof(InflateLds<10, 8, uint16_t>), s, comp,
+    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64), 0, s, comp,
                        nwords, jobs, dicts, out, res, njobs, blk, nullptr);
 #ifdef PPG_IX_STATS
     {
