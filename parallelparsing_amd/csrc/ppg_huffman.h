@@ -20,8 +20,8 @@
 //          [3:0] code length L, [9:5] L + length extra bits, [14:10] length extra bits, [15] set,
 //          [31:16] length base.  (r03: the decoder selects a literal's word instead of assembling
 //          it from fields, ~10 VALU fewer per candidate.)
-//  dist:   [3:0] L2 (0 = bit-serial), [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base - 1
-//          (the token word's field is distance - 1)
+//  dist:   [3:0] L2, [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base - 1 (the token
+//          word's field is distance - 1); all ones = decode bit-serially (its sign bit is the test)
 //  code-length code: [3:0] L, [15:8] symbol
 
 __constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -55,14 +55,14 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int k
         const uint32_t x = c_lext[sym - 257];
         return len | ((len + x) << 5) | (x << 10) | 0x8000u | ((uint32_t)c_lbase[sym - 257] << 16);
     }
-    if (sym >= 30) return 0u;
+    if (sym >= 30) return ~0u;
     const uint32_t x = c_dext[sym];
     return len | ((len + x) << 5) | (x << 10) | ((uint32_t)(c_dbase[sym] - 1) << 16);
 }
 
 // Builds a canonical-Huffman root table of 2^TB entries from n code lengths (all 64 lanes).
-// Codes longer than TB (and unused patterns of an incomplete code) get the bit-serial entry (0, or
-// the special token word in a litlen table) -> bit-serial path,
+// Codes longer than TB (and unused patterns of an incomplete code) get the bit-serial entry (0; the
+// special token word in a litlen table, all ones in a distance table) -> bit-serial path,
 // which decodes bit-by-bit from count[]/sorted[].  Validity follows zlib 1.2.11 inflate_table:
 // over-subscribed -> error; incomplete -> error unless exactly one code of length 1 (not for
 // the code-length code); no codes at all -> accepted (decoding then fails).  Returns 0 / -1.
@@ -126,7 +126,8 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, Canon *c
     for (int e0 = 0; e0 < (1 << TB); e0 += 64) {   // uniform trip count (see ppg_inflate_kernel)
         const int e = e0 + lane;
         // not found (longer than TB, or an unused pattern of an incomplete code): bit-serial
-        uint32_t code = 0, first = 0, index = 0, entry = kind == TAB_LIT ? PPG_SPECIAL_TOKEN : 0u;
+        uint32_t code = 0, first = 0, index = 0,
+                 entry = kind == TAB_LIT ? PPG_SPECIAL_TOKEN : kind == TAB_DST ? ~0u : 0u;
         bool found = false;
 #pragma unroll 1
         for (int l = 1; l <= TB; l++) {

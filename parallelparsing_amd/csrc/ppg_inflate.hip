@@ -79,8 +79,9 @@
 
 template <int RB, int LBT, typename RingT = uint8_t>
 struct __attribute__((aligned(16))) InflateLds {
-    RingT ring[1u << RB];          // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1)
+    // first: the decode's five-word reads address it with ds_read2 offsets (8-bit dword fields)
     uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
+    RingT ring[1u << RB];          // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1)
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LBT];
         uint32_t cl[1 << CB];
@@ -498,17 +499,18 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     const uint32_t xs = e >> 10;
     const uint32_t mlen = (e >> 16) + __builtin_amdgcn_ubfe(r1, 0u, xs);
     const uint32_t y = __builtin_amdgcn_alignbit(0u, r1, xs);      // past the extra bits
-    const uint32_t d = dst[__builtin_amdgcn_ubfe(r1, xs, (uint32_t)DB)];
+    const uint32_t d = dst[y & ((1u << DB) - 1)];
     // distance - 1 = (base - 1) + the extra bits after the distance code (d[4:0] = L2, (d >> 10)[4:0] = extra)
     const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(y, d, d >> 10);
     const uint32_t tb = ((e >> 5) & 31) + ((d >> 5) & 31);
     const uint32_t tlen = tb | (mlen << 8) | (dm1 << 17);
-    const uint32_t t2 = (d & 15u) ? tlen : PPG_SPECIAL_TOKEN;             // bit-serial distance code
-    // e for a literal / special entry, t2 for a length symbol's (bit 15): one v_bfi on the sign-
-    // extended flag (a ?: here became a divergent branch -- exec juggling costs more than the VALU --
-    // or, written as masks, three instructions)
+    // e for a literal / special entry, tlen for a length symbol's (bit 15) -- unless its distance
+    // code is bit-serial (entry all ones): v_bfi on sign-extended flags (a ?: here became a divergent
+    // branch -- exec juggling costs more than the VALU -- or, written as masks, three instructions)
     const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);
-    uint32_t tok;
+    const uint32_t sd = (uint32_t)((int32_t)d >> 31);
+    uint32_t t2, tok;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(t2) : "v"(sd), "v"(PPG_SPECIAL_TOKEN), "v"(tlen));
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tok) : "v"(lm), "v"(t2), "v"(e));
     return tok;
 }
