@@ -1047,9 +1047,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     const bool fo = far && p >= 0;
                     const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
 #endif
-                    val = fo ? (w >> (8 * (q & 3))) & (IX ? 0xFFFFu : 255u) : val;
+                    // (bit-field offset q << 3: the instruction reads its low 5 bits, 8 * (q & 3))
+                    val = fo ? __builtin_amdgcn_ubfe(w, q << 3, IX ? 16u : 8u) : val;
                     const bool fd = far && p < 0;
-                    const uint64_t dm = __ballot(fd);
+                    const uint64_t dm = fm & __ballot(p < 0);   // (a ballot of fd itself went through two VALU)
                     if (PPG_COLD(dm)) {   // rare: the chunk's first 32 KiB
                         uint32_t db;
                         if constexpr (IX) db = 32768u + (uint32_t)p;          // the history symbol itself
