@@ -851,7 +851,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         // returns the token words placed at their output offsets, the output bytes the round's
         // tokens cover (off), the bit advance (adv) and whether it stopped at a special token
         struct Round { uint32_t vtin, off, adv; bool spec; };
+        // the five stream words a lane decodes from at bit bp (st_enter made their segments resident)
+        struct Words { uint32_t x0, x1, x2, x3, x4; };
+        auto words = [&](uint32_t bp) -> Words {
+            const uint32_t o = (bp & 31) + (uint32_t)lane;                      // 0..94
+            const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
+            return Words{sw[0], sw[1], sw[2], sw[3], sw[4]};
+        };
+#ifdef PPG_NO_WORD_PREFETCH
         auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos) -> Round {
+#else
+        auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos, const Words &W) -> Round {
+#endif
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t vtin = 0;
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
@@ -861,10 +872,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 asm volatile("s_setprio " PPG_STR(PPG_DEC_PRIO));
 #endif
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
-                // ring; st_enter already made the segment resident)
+                // ring, read during the previous round's emit)
                 const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
-                const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
-                const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2], x3 = sw[3], x4 = sw[4];
+#ifdef PPG_NO_WORD_PREFETCH
+                const Words W = words(bp);
+#endif
+                const uint32_t x0 = W.x0, x1 = W.x1, x2 = W.x2, x3 = W.x3, x4 = W.x4;
                 // speculative tokens at every bit offset of the 128-bit span (two per lane)
                 const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
                                                      __builtin_amdgcn_alignbit(x2, x1, o), (uint32_t)lane);
@@ -970,11 +983,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             return Round{vtin, off, s, spec};
         };
 
+#ifndef PPG_NO_WORD_PREFETCH
+        st_enter(r, S.stream, bp >> 10, lane);
+        Words W = words(bp);
+#endif
         for (;;) {
             // ---- one round: decode + walk, then one output byte per lane ----
             PPG_STAMP(t0);
+#ifdef PPG_NO_WORD_PREFETCH
             st_enter(r, S.stream, bp >> 10, lane);
             const Round R = decode(bp, cn, cw, pos);
+#else
+            const Round R = decode(bp, cn, cw, pos, W);
+            // the next round's stream words, read now: their LDS latency overlaps this round's
+            // emit instead of opening the next round's chain of dependent LDS reads (r03)
+            st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+            W = words(bp + R.adv);
+#endif
 #ifdef PPG_STAMPS
             const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
             if (st_w0 < t0) st_w0 = t1;   // no walk this round
@@ -1167,6 +1192,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
+#ifndef PPG_NO_WORD_PREFETCH
+            st_enter(r, S.stream, bp >> 10, lane);
+            W = words(bp);
+#endif
 #ifdef PPG_SPEC_PRIO
             asm volatile("s_setprio 0");
 #endif
