@@ -16,10 +16,12 @@
 //  litlen: a literal's entry is its finished token word (the decoder's format: [7:0] bits = L,
 //          [16:8] bytes = 1, [31:17] 0x100 | byte), and an entry to decode bit-serially (end-of-
 //          block, invalid symbol, or a code longer than the root table) the special token word
-//          (bits 128, bytes 0, field 0x100); both have bit 15 clear.  A length symbol's entry:
-//          [3:0] code length L, [9:5] L + length extra bits, [14:10] length extra bits, [15] set,
-//          [31:16] length base.  (r03: the decoder selects a literal's word instead of assembling
-//          it from fields, ~10 VALU fewer per candidate.)
+//          (bits 128, bytes 0, field 0x100); both have bit 6 clear.  A length symbol's entry:
+//          [3:0] code length L, [6] set, [15:8] L + length extra bits, [24:16] length base, so
+//          e >> 8 is the token word's bits + bytes part before the extra bits' value, and
+//          ((e >> 8) - e)[4:0] the number of extra bits.  (r03: the decoder selects a literal's word
+//          instead of assembling it from fields, ~10 VALU fewer per candidate; r03 v4: this length
+//          layout, 3 VALU fewer per candidate.)
 //  dist:   [3:0] L2, [9:5] L2 + extra bits, [14:10] extra bits, [31:16] base - 1 (the token
 //          word's field is distance - 1); all ones = decode bit-serially (its sign bit is the test)
 //  code-length code: [3:0] L, [15:8] symbol
@@ -53,7 +55,7 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t sym, uint32_t len, int k
         if (sym < 256) return len | (1u << 8) | ((0x100u | sym) << 17);
         if (sym == 256 || sym >= 286) return PPG_SPECIAL_TOKEN;
         const uint32_t x = c_lext[sym - 257];
-        return len | ((len + x) << 5) | (x << 10) | 0x8000u | ((uint32_t)c_lbase[sym - 257] << 16);
+        return len | 0x40u | ((len + x) << 8) | ((uint32_t)c_lbase[sym - 257] << 16);
     }
     if (sym >= 30) return ~0u;
     const uint32_t x = c_dext[sym];

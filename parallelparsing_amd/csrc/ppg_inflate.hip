@@ -427,6 +427,13 @@ __device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) 
     asm volatile(PPG_FAR_PAD "global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
     return v;
 }
+// the byte itself (DecompressAll's emit): no alignment mask, no bit-field extract (r03 v4:
+// 707 -> 698.5 ms per 50 GB step, same-box A/B)
+__device__ __forceinline__ uint32_t far_load_u8(const uint8_t *base, uint32_t off) {
+    uint32_t v;
+    asm volatile(PPG_FAR_PAD "global_load_ubyte %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+    return v;
+}
 
 // far_load in two halves (PPG_FAR_SPLIT): the load, and the wait that hands its result over.  The
 // value is an in/out operand of the wait, so nothing reads it before the load has landed.
@@ -494,20 +501,16 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     // a literal's (or a special code's) root entry is already its token word; only a length
     // symbol's entry (bit 15) is assembled from the two tables (ppg_huffman.h, r03)
     const uint32_t e = lit[lo & ((1u << LBT) - 1)];
-    const uint32_t r1 = __builtin_amdgcn_alignbit(hi, lo, e);      // past the litlen code (e[4:0] = L)
-    // xs[4:0] = the length's extra bits: shift / bit-field operands use only their low 5 bits
-    const uint32_t xs = e >> 10;
-    const uint32_t mlen = (e >> 16) + __builtin_amdgcn_ubfe(r1, 0u, xs);
-    const uint32_t y = __builtin_amdgcn_alignbit(0u, r1, xs);      // past the extra bits
+    // length entry: e >> 8 = [7:0] L + x, [16:8] length base; (e >> 8) - e has x in its low 5 bits
+    const uint32_t e2 = e >> 8;
+    const uint32_t xs = e2 - e;
+    const uint32_t y = __builtin_amdgcn_alignbit(hi, lo, e2);      // past the code and its extra bits
+    uint32_t tke;   // bits and bytes of the length (one v_lshl_add; the compiler split it in two)
+    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(tke) : "v"(__builtin_amdgcn_ubfe(lo, e, xs)), "v"(e2));
     const uint32_t d = dst[y & ((1u << DB) - 1)];
-    // distance - 1 = (base - 1) + the extra bits after the distance code (d[4:0] = L2, (d >> 10)[4:0] = extra)
     const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(y, d, d >> 10);
-    const uint32_t tb = ((e >> 5) & 31) + ((d >> 5) & 31);
-    const uint32_t tlen = tb | (mlen << 8) | (dm1 << 17);
-    // e for a literal / special entry, tlen for a length symbol's (bit 15) -- unless its distance
-    // code is bit-serial (entry all ones): v_bfi on sign-extended flags (a ?: here became a divergent
-    // branch -- exec juggling costs more than the VALU -- or, written as masks, three instructions)
-    const uint32_t lm = (uint32_t)((int32_t)(e << 16) >> 31);
+    const uint32_t tlen = tke + ((d >> 5) & 31) + (dm1 << 17);
+    const uint32_t lm = (uint32_t)((int32_t)(e << 25) >> 31);       // bit 6: a length symbol
     const uint32_t sd = (uint32_t)((int32_t)d >> 31);
     uint32_t t2, tok;
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(t2) : "v"(sd), "v"(PPG_SPECIAL_TOKEN), "v"(tlen));
@@ -1068,12 +1071,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     const uint32_t w = far_wait(fw);
 #else
                     const int32_t p = (int32_t)pos + jj;
-                    const uint32_t q = IX ? 2u * ((uint32_t)p & IX_RING_MASK) : oa + (uint32_t)p;   // byte offset
                     const bool fo = far && p >= 0;
-                    const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
+                    if constexpr (IX) {
+                        const uint32_t q = 2u * ((uint32_t)p & IX_RING_MASK);
+                        const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
+                        val = fo ? __builtin_amdgcn_ubfe(w, q << 3, 16u) : val;
+                    } else {
+                        // one byte load at ob + oa + p (pos + oa is wave-uniform)
+                        const uint32_t b = far_load_u8(ob, fo ? (uint32_t)jj + (pos + oa) : 0u);
+                        val = fo ? b : val;
+                    }
 #endif
+#ifdef PPG_FAR_SPLIT
                     // (bit-field offset q << 3: the instruction reads its low 5 bits, 8 * (q & 3))
                     val = fo ? __builtin_amdgcn_ubfe(w, q << 3, IX ? 16u : 8u) : val;
+#endif
                     const bool fd = far && p < 0;
                     const uint64_t dm = fm & __ballot(p < 0);   // (a ballot of fd itself went through two VALU)
                     if (PPG_COLD(dm)) {   // rare: the chunk's first 32 KiB
