@@ -80,7 +80,11 @@
 template <int RB, int LBT, typename RingT = uint8_t>
 struct __attribute__((aligned(16))) InflateLds {
     // first: the decode's five-word reads address it with ds_read2 offsets (8-bit dword fields)
+#ifdef PPG_WORDS6
+    uint32_t stream[136];          // compressed words: segment g (32 words) at slot g & 3; [128,134) mirror [0,6)
+#else
     uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
+#endif
     RingT ring[1u << RB];          // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1)
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LBT];
@@ -166,7 +170,11 @@ __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint
     const uint32_t i = min(g * 32 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
     if (lane < 32) lds_dma_dword(r.base + i, stream + (g & 3) * 32);
     // slot 0's first words again after slot 3, so a lane's consecutive words never wrap
+#ifdef PPG_WORDS6
+    if ((g & 3) == 0 && lane < 6) lds_dma_dword(r.base + i, stream + 128);
+#else
     if ((g & 3) == 0 && lane < 4) lds_dma_dword(r.base + i, stream + 128);
+#endif
 }
 
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
@@ -595,6 +603,15 @@ __device__ __forceinline__ void walk_asm_pair(uint32_t vt, uint32_t vt2, uint32_
 //             start until a block ends at or past stop_bit, recording every block end.
 // SGPR budget: a wave holds ceil(sgpr/16)*16 + 16 of the SIMD's 800 SGPRs, so .sgpr_count <= 80 is
 // needed for 8 waves per SIMD (97 gives 6; MI355X_MICROARCH.md, occupancy formula)
+// r03 v4: the token rounds as an inner loop with one latch, and the emit's token-start address as
+// one v_mad_i32_i24 -- together 694.5 -> 682.2 ms per 50 GB step (each alone: 695.1 / 701.0;
+// profiles/r03_ab_latch_sj.txt).  PPG_TWO_EXITS / PPG_SJ_SHIFT build the previous forms.
+#if !defined(PPG_TWO_EXITS) && !defined(PPG_ONE_LATCH)
+#define PPG_ONE_LATCH
+#endif
+#if !defined(PPG_SJ_SHIFT) && !defined(PPG_SJ_MAD)
+#define PPG_SJ_MAD
+#endif
 #ifndef PPG_NUM_SGPR
 #define PPG_NUM_SGPR 80
 #endif
@@ -858,7 +875,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         struct Words { uint32_t x0, x1, x2, x3, x4; };
         auto words = [&](uint32_t bp) -> Words {
             const uint32_t o = (bp & 31) + (uint32_t)lane;                      // 0..94
+#ifdef PPG_WORDS6
+            // the wrap applied to the uniform part only: a lane's words end at most at 127 + 2 + 4
+            const uint32_t *sw = S.stream + (((bp >> 5) & 127) + (o >> 5));
+#else
             const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
+#endif
             return Words{sw[0], sw[1], sw[2], sw[3], sw[4]};
         };
 #ifdef PPG_NO_WORD_PREFETCH
@@ -991,6 +1013,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         Words W = words(bp);
 #endif
         for (;;) {
+#ifdef PPG_ONE_LATCH
+          // the token rounds as an inner loop with ONE latch (not special, output left): the two
+          // exits of the plain form made the compiler merge them through an exit-selector register
+          bool spec_ = false;
+          do {
+#endif
             // ---- one round: decode + walk, then one output byte per lane ----
             PPG_STAMP(t0);
 #ifdef PPG_NO_WORD_PREFETCH
@@ -1024,8 +1052,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
             // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
             {
+#ifdef PPG_SJ_MAD
+                // 4 * (63 - clz) in one v_mad_i32_i24 (the compiler's form: shift + xor)
+                uint32_t sj4;
+                asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
+                const uint32_t inf = bperm(sj4, R.vtin);
+#else
                 const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
                 const uint32_t inf = bperm(sj << 2, R.vtin);
+#endif
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
 #ifdef PPG_FAR_SPLIT
                 // the far load goes out before the ring read, so the two latencies overlap
@@ -1165,10 +1200,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
             st_w0 = 0;
 #endif
+#ifdef PPG_ONE_LATCH
+            spec_ = R.spec;
+          } while (PPG_HOT(!spec_ && pos < len));
+            if (!spec_) break;
+#else
             if (PPG_HOT(!R.spec)) {
                 if (PPG_HOT(pos < len)) continue;
                 break;
             }
+#endif
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
 #ifdef PPG_SPEC_PRIO
