@@ -890,7 +890,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #endif
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t vtin = 0;
+#ifdef PPG_CARRY_ALWAYS
+            vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);   // cw = 0 without a carry
+#else
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
+#endif
             bool spec = false;
             if (off < min(64u, len - pos)) {
 #ifdef PPG_DEC_PRIO
@@ -1180,6 +1184,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
                 cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
             }
+#ifdef PPG_CARRY_ALWAYS
+            else cw = 0;
+#endif
             pos += rout;
             if (PPG_COLD(pos >= fl_next)) {
 #ifdef PPG_FLUSH_PRIO
