@@ -507,7 +507,7 @@ template <int LBT>
 __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32_t *dst, uint32_t lo, uint32_t hi,
                                                uint32_t lane) {
     // a literal's (or a special code's) root entry is already its token word; only a length
-    // symbol's entry (bit 15) is assembled from the two tables (ppg_huffman.h, r03)
+    // symbol's entry (bit 6) is assembled from the two tables (ppg_huffman.h, r03)
     const uint32_t e = lit[lo & ((1u << LBT) - 1)];
     // length entry: e >> 8 = [7:0] L + x, [16:8] length base; (e >> 8) - e has x in its low 5 bits
     const uint32_t e2 = e >> 8;
