@@ -307,7 +307,13 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     const uint64_t end_bits = 8ull * (uint64_t)(len - 8);   // no block header starts in the trailer
     // default ~65k pieces (768 KiB for a 50 GB member: 3.41 s vs 3.72 s at 16k pieces, r02 --ix-piece-kib
     // sweep -- pass 2's batches hold several generations of waves; smaller pieces cost more setup)
-    if (piece_bytes <= 0) piece_bytes = std::min<int64_t>(4 << 20, std::max<int64_t>(256 << 10, len / 65536));
+    if (piece_bytes <= 0) {
+        piece_bytes = std::min<int64_t>(4 << 20, std::max<int64_t>(256 << 10, len / 65536));
+        // a caller-sized pass-2 buffer holds ~4 output bytes per compressed byte: at most
+        // capacity / 32768 per piece keeps ~8k pieces (a generation of waves) per batch
+        // (16 GiB: 512 KiB pieces, 2.18 -> 2.02 s for the 50 GB member, r03 v5 sweep)
+        if (out_capacity > 0) piece_bytes = std::max<int64_t>(256 << 10, std::min<int64_t>(piece_bytes, out_capacity / 32768));
+    }
     const uint64_t pbits = 8ull * (uint64_t)piece_bytes;
 
     // ---- 1. candidate block starts ----
