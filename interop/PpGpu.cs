@@ -10,12 +10,25 @@ namespace ParallelParsing.Interop;
 
 public static class PpgStatus
 {
-    public const int IndexOutOfRange = -50;   // C# IndexOutOfRangeException (SURVEY Q4)
+    public const int IndexOutOfRange = -50;   // C# IndexOutOfRangeException (SURVEY Q4, Core.cs:93)
     public const int IoError = -51;
     public const int ArgError = -52;
     public const int Unsupported = -53;
     public const int DeviceError = -100;
     public const int NoDevice = -101;
+}
+
+/// <summary>A libppgpu failure that is not a zlib result (PpgStatus codes other than
+/// IndexOutOfRange): bad arguments, unreadable files, unsupported input, device errors.  zlib's
+/// results keep the reference's ZException (Interop/Conventions.cs:33-41).</summary>
+public class PpgException : Exception
+{
+    public int Code { get; }
+
+    public PpgException(int code, string what) : base($"libppgpu: {what} ({code})")
+    {
+        Code = code;
+    }
 }
 
 [StructLayout(LayoutKind.Sequential)]
@@ -124,8 +137,32 @@ internal static unsafe class PpGpu
     [DllImport(Lib)] public static extern nint ppg_version();
     [DllImport(Lib)] public static extern nint ppg_build_id();
 
+    // Status -> exception, as the reference's callers do (Core.cs:31-34, :68-74, :178-179): zlib's
+    // ZResult codes (Conventions.cs:9-20) become ZException; the IndexOutOfRange that CreateIndex's
+    // offset buffer throws in the reference (Core.cs:93, SURVEY Q4) stays IndexOutOfRangeException;
+    // every library code becomes a PpgException carrying it.  Every PPG_* status of ppgpu.h has a
+    // case here (tests/test_interop_cs.py); an unknown code is a PpgException too, never a ZResult
+    // cast of a value the enum does not define.
     public static void Check(int rc)
     {
-        if (rc != 0) throw new ZException((ZResult)rc);   // as Core.cs:68-74 / :178-179
+        switch (rc)
+        {
+            case 0: return;                                                       // PPG_OK
+            case 1: throw new ZException(ZResult.STREAM_END);                     // PPG_STREAM_END
+            case 2: throw new ZException(ZResult.NEED_DICT);                      // PPG_NEED_DICT
+            case -1: throw new ZException(ZResult.ERRNO);                         // PPG_ERRNO
+            case -2: throw new ZException(ZResult.STREAM_ERROR);                  // PPG_STREAM_ERROR
+            case -3: throw new ZException(ZResult.DATA_ERROR);                    // PPG_DATA_ERROR
+            case -4: throw new ZException(ZResult.MEM_ERROR);                     // PPG_MEM_ERROR
+            case -5: throw new ZException(ZResult.BUF_ERROR);                     // PPG_BUF_ERROR
+            case -6: throw new ZException(ZResult.VERSION_ERROR);                 // PPG_VERSION_ERROR
+            case -50: throw new IndexOutOfRangeException();                       // PPG_INDEX_OUT_OF_RANGE
+            case -51: throw new PpgException(rc, "I/O error");                    // PPG_IO_ERROR
+            case -52: throw new PpgException(rc, "invalid argument");             // PPG_ARG_ERROR
+            case -53: throw new PpgException(rc, "unsupported input");            // PPG_UNSUPPORTED
+            case -100: throw new PpgException(rc, "device error");                // PPG_DEVICE_ERROR
+            case -101: throw new PpgException(rc, "no gfx950 device");            // PPG_NO_DEVICE
+            default: throw new PpgException(rc, "unknown status");
+        }
     }
 }

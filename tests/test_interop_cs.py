@@ -142,3 +142,54 @@ def test_type_check_catches_drift():
     assert "int" not in _allowed("int64_t")
     assert "nint" not in _allowed("ppg_index**")
     assert "byte*" not in _allowed("int64_t*")
+
+
+# ---- status mapping ----
+def _c_status_codes():
+    """Every status #define of ppgpu.h: name -> value (sizes such as PPG_WINSIZE excluded)."""
+    h = _read("include", "ppgpu.h")
+    out = {}
+    for name, val in re.findall(r"#define\s+(PPG_\w+)\s+\(?(-?\d+)\)?", h):
+        if name in ("PPG_WINSIZE", "PPG_CHUNK", "PPG_COMM_ID_BYTES"):
+            continue
+        out[name] = int(val)
+    return out
+
+
+def _cs_check_cases():
+    """PpGpu.Check's switch: value -> (exception thrown or 'return', the PPG_ name in its comment)."""
+    cs = _read("interop", "PpGpu.cs")
+    body = cs[cs.index("public static void Check(int rc)"):]
+    body = body[:body.index("default:")]
+    out = {}
+    for val, act, name in re.findall(r"case\s+(-?\d+):\s*(return|throw new \w+)[^\n]*//\s*(PPG_\w+)", body):
+        out[int(val)] = ("return" if act == "return" else act.split()[-1], name)
+    return out
+
+
+def test_check_maps_every_status_of_the_header():
+    codes, cases = _c_status_codes(), _cs_check_cases()
+    assert len(codes) >= 15
+    assert sorted(cases) == sorted(codes.values())
+    for name, val in codes.items():
+        exc, cname = cases[val]
+        assert cname == name, (val, cname, name)
+        if val == 0:
+            assert exc == "return"
+        elif -6 <= val <= 2:            # zlib's ZResult values (Interop/Conventions.cs:9-20)
+            assert exc == "ZException", name
+        elif name == "PPG_INDEX_OUT_OF_RANGE":   # Core.cs:93 throws IndexOutOfRangeException
+            assert exc == "IndexOutOfRangeException"
+        else:
+            assert exc == "PpgException", name
+    cs = _read("interop", "PpGpu.cs")
+    assert "(ZResult)rc" not in cs   # no cast of a library code into the zlib enum
+    assert re.search(r"default:\s*throw new PpgException", cs)
+
+
+def test_status_class_lists_the_library_codes():
+    cs = _read("interop", "PpGpu.cs")
+    body = cs[cs.index("public static class PpgStatus"):]
+    body = body[:body.index("}")]
+    vals = {int(v) for v in re.findall(r"=\s*(-\d+);", body)}
+    assert vals == {v for v in _c_status_codes().values() if v <= -50}
