@@ -283,6 +283,66 @@ def ingest_run(tf, ix, dev, threads, piece_gib=8.0, enum_gib=0.0):
             os.remove(path)
 
 
+def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16, max_chunks=1024, side=16):
+    """README "Decompress" (ppg_decompress_chunk, thread safe): T host threads calling it on one ctx,
+    each for its own chunk at a time, as the reference's one task per chunk does
+    (BatchedFASTQ.cs:62-77).  Slices from host memory, bytes + descriptors back into host buffers;
+    the per-chunk record counts are checked against the timed DecompressAll run's.  Twice: with the
+    plain index (one wave per chunk) and with side points attached (up to `side` waves per chunk)."""
+    import threading
+    import parallelparsing_amd as pp
+    nmax = min(max_chunks, len(counts), per_thread * max(threads_list))
+    slices = [np.frombuffer(tf.file_bytes(int(tf.p_input[k]) - 1, int(tf.p_input[k + 1])), np.uint8)
+              for k in range(nmax)]
+    plain = tf.index(0, nmax + 1)
+    split = tf.index(0, nmax + 1).set_side_points(*tf.side_points(0, nmax + 1, side))
+
+    def leg(ix, T):
+        n = min(nmax, per_thread * T)
+        before = dev.decompress_chunk_stats()
+        nxt = [0]
+        lock = threading.Lock()
+        got = np.zeros(n, np.int64)
+        errs = []
+
+        def work():
+            try:
+                while True:
+                    with lock:
+                        k = nxt[0]
+                        nxt[0] += 1
+                    if k >= n:
+                        return
+                    _, _, rec = pp.Core.ExtractDeflateIndex(slices[k], ix, k, device=dev, with_records=True)
+                    got[k] = len(rec)
+            except Exception as e:   # noqa: BLE001 - re-raised below
+                errs.append(e)
+        th = [threading.Thread(target=work) for _ in range(T)]
+        t = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        sec = time.perf_counter() - t
+        if errs:
+            raise errs[0]
+        assert (got == counts[:n]).all(), "ppg_decompress_chunk record counts differ from DecompressAll's"
+        after = dev.decompress_chunk_stats()
+        calls, launches = after["calls"] - before["calls"], after["launches"] - before["launches"]
+        return {"chunks": n, "records_per_s": float(got.sum()) / sec, "chunks_per_s": n / sec,
+                "ms_per_call": sec * 1e3 * T / n, "seconds": sec, "launches": launches,
+                "chunks_per_launch": calls / max(1, launches)}
+
+    leg(plain, 8)   # warm: the slots' buffers grow to their working size
+    out = {f"T{T}": leg(plain, T) for T in threads_list}
+    out["side_points"] = {f"T{T}": leg(split, T) for T in threads_list}
+    out["note"] = ("ppg_decompress_chunk from T host threads on one ctx (concurrent calls combined into shared "
+                   "launches, two launch slots); plain index: one wave per chunk; side_points: the same chunks with "
+                   f"<= {side} waves each (ppg_index_set_side_points); host slices in, bytes + descriptors out; not "
+                   "the bench value")
+    return out
+
+
 def create_index_run(tf, args, dev):
     """GPU CreateIndex (ppg_index_build_gpu) over the whole member resident in HBM, checked Point by
     Point against the member's exactly derived index, beside the host zlib CreateIndex (the
@@ -354,8 +414,9 @@ def paired_run(args, dev, world=1, rank=0, xdev=None):
     record's spot key extracted on the GPU, Q1 duplicates dropped and the pair invariant checked
     (paired.PairedFASTQ's path).  On N ranks each rank decodes its contiguous chunk range of BOTH
     files (dist.partition_chunks per file); the files' record ranges do not line up across ranks,
-    so the pair check is a real exchange: paired.distributed_pair_check all-gathers the counts and
-    moves every spot key to the rank owning its pair number (all_to_all, RCCL over xGMI).  Size per
+    so the pair check is a real exchange: ppg_pairs_check (C ABI) all-gathers the counts and moves
+    every spot key to the rank owning its pair number (ppg_comm_alltoallv: RCCL ncclSend/ncclRecv
+    over xGMI; the host transport in the one-GPU rehearsal).  Size per
     file: --paired-repeats segments (default 102: configs[4]'s ~25 GB of gzip per file at any N).
     The spot keys are extracted per output batch while it is resident (ppg_shard_set_keys), so a
     rank's range may decode in several batches of --paired-out-gib: on one GPU the two ~103 GB
@@ -403,6 +464,13 @@ def paired_run(args, dev, world=1, rank=0, xdev=None):
         f"{shards[0].batches} + {shards[1].batches} output batches, setup {setup_s:.1f}s")
 
     import threading
+    pairs = paired.Pairs()
+    comm, via = (None, "ppg_pairs_check on one GPU")
+    if world > 1:
+        comm, via = make_comm(ctxs[0], world, rank, backend, xdev)
+        if comm is None:
+            raise RuntimeError(f"paired run needs the library's communicator: {via}")
+        via = "ppg_pairs_check: keys to pair owners by ppg_comm_alltoallv (" + via.split(" over ")[-1] + ")"
 
     def step():
         errs = []
@@ -417,20 +485,12 @@ def paired_run(args, dev, world=1, rank=0, xdev=None):
             x.start()
         for x in th:
             x.join()
-        if world > 1:   # a failing rank must not leave the others in the key exchange
-            f = torch.tensor([len(errs)], dtype=torch.int64, device=xdev)
-            dist.all_reduce(f)
-            if int(f.item()):
-                raise errs[0] if errs else RuntimeError("DecompressAll failed on another rank")
-        elif errs:
+        # every rank joins the check: a rank whose decode failed reports it there, and every rank
+        # raises the first failing rank's status (ppg_pairs_check's status gather)
+        res = pairs.check(shards[0], shards[1], comm)
+        if errs:
             raise errs[0]
-        keys = [paired.dedup(paired.shard_keys(sh))[0] for sh in shards]
-        if world == 1:
-            return paired.check_pairs(keys[0], keys[1])
-        npairs, bad = paired.distributed_pair_check(keys[0].to(xdev), keys[1].to(xdev))
-        if bad:
-            raise ValueError(f"{bad} mismatched pairs")
-        return npairs
+        return paired.require_pairs(res)
 
     import torch.distributed as dist
     for _ in range(args.warmup):
@@ -469,7 +529,7 @@ def paired_run(args, dev, world=1, rank=0, xdev=None):
                    "pairs": npairs, "gz_bytes": [tf.file_len for tf in tfs], "decompressed_bytes": text,
                    "output_batches_per_file": [sh.batches for sh in shards],
                    "keys": "per output batch while resident (ppg_shard_set_keys)",
-                   "pair_check": "on-device" if world == 1 else "all_to_all of spot keys to pair owners",
+                   "pair_check": via,
                    "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
         "decompressed_MBps": text * args.steps / elapsed / 1e6,
         "setup_s": {"input": round(args.input_seconds, 2), "shards": round(setup_s, 2)},
@@ -487,14 +547,21 @@ def auto_split(args, slots, chunks):
     --split S > 0: every chunk.  --split 0 (auto): a rank holding less than one generation of
     resident waves (CUs x 32; --split-gens) splits every chunk, into enough waves for ~6
     generations and at least --tail-split (at most 64: in practice every inner block start, ~15 per
-    10k-record chunk); a larger rank splits only its last half-generation (--tail-gens) into
-    --tail-split = 8, so the launch's tail drains in an eighth of a chunk's time.  Measured on one
-    MI355X for the N = 1 step and the N = 2/4/8 strong-scaling shares."""
+    10k-record chunk); a larger rank splits its last --tail-gens generations into --tail-split = 8,
+    so the launch's tail drains in an eighth of a chunk's time.  --tail-gens auto: half a generation
+    once the rank holds 2.5 generations or more (its waves' start times have spread out by the last
+    generation), else one whole generation: with 1.6 generations (N = 4) the chunks left whole then
+    all start at once, beside the pieces, instead of a last 0.1 generation of whole chunks starting
+    when the first generation ends (r04: the N = 4 share 188.9 -> 175.6 ms).  Measured on one MI355X
+    for the N = 1 step and the N = 2/4/8 strong-scaling shares."""
     if args.split > 0:
         return args.split, chunks
     if chunks < getattr(args, "split_gens", 1) * slots:
         return int(min(64, max(args.tail_split, -(-6 * slots // max(1, chunks))))), chunks
-    return args.tail_split, min(chunks, int(args.tail_gens * slots))
+    gens = args.tail_gens
+    if gens in (None, "auto"):
+        gens = 0.5 if chunks >= 2.5 * slots else 1.0
+    return args.tail_split, min(chunks, int(float(gens) * slots))
 
 
 def tail2_split(args, slots, ksplit):
@@ -636,8 +703,9 @@ def main():
                          "chunk; a larger one splits its last --tail-gens generations into --tail-split waves")
     ap.add_argument("--tail-split", type=int, default=8,
                     help="--split 0 on a large rank: waves per chunk for its last generation of chunks (1 = off)")
-    ap.add_argument("--tail-gens", type=float, default=0.5,
-                    help="--split 0 on a large rank: how many generations of its last chunks to split")
+    ap.add_argument("--tail-gens", default="auto",
+                    help="--split 0 on a large rank: how many generations of its last chunks to split (auto: 0.5 "
+                         "from 2.5 generations of chunks up, else 1)")
     ap.add_argument("--split", type=int, default=0,
                     help="decode each chunk as up to S waves, split at inner deflate block starts "
                          "(ppg_shard_set_split; side points from the member's block list); 1 = one wave per chunk; "
@@ -656,6 +724,9 @@ def main():
     ap.add_argument("--no-enumerate", action="store_true",
                     help="skip the enumerator leg (N = 1, after the ingest leg): every record's bytes and descriptor "
                          "landed in host memory through ppg_cursor (reported under 'enumerate', never as value)")
+    ap.add_argument("--no-chunk-api", action="store_true",
+                    help="skip the per-chunk Decompress leg (N = 1): ppg_decompress_chunk from 1/8/64 host threads "
+                         "(reported under 'decompress_chunk', never as value)")
     ap.add_argument("--enum-batch-gib", type=float, default=8.0, help="enumerator leg: text per cursor batch (GiB)")
     args = ap.parse_args()
     if args.seg_records is None:   # the paired files keep 1 GB segments: two members must fit one GPU
@@ -886,6 +957,11 @@ def main():
                 line["enumerate"] = enum
         except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
             line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0 and world == 1 and args.workload == "50gb" and not args.no_chunk_api and args.share == 1:
+        try:
+            line["decompress_chunk"] = decompress_chunk_run(tf, ctx, r["records"])
+        except (AssertionError, RuntimeError, pp.PpgError) as e:
+            line["decompress_chunk"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(tf, ix_out, ix_in, nchunks, usable_cpus())
     if rank == 0:

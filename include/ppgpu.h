@@ -14,7 +14,9 @@
  *  - no exceptions cross the ABI; caller-owned buffers are pinned by the caller (as Core.cs:162,
  *    171 pins Memory<byte>) and never retained; library-owned objects have explicit _free/_close;
  *  - one ppg_ctx per GPU; a ctx is used by one host thread at a time (the reference's
- *    per-call ZStream, Core.cs:136, is likewise single-threaded).
+ *    per-call ZStream, Core.cs:136, is likewise single-threaded) -- except ppg_decompress_chunk,
+ *    the README's thread-safe "Decompress", which any number of threads may call on one ctx at
+ *    once (alongside the one thread using the ctx's other entry points).
  */
 #ifndef PPGPU_H
 #define PPGPU_H
@@ -73,6 +75,11 @@ int ppg_index_build_gpu_side(ppg_ctx *ctx, const void *gz, int64_t gz_len, int g
 int ppg_index_side_count(const ppg_index *ix);
 /* copies the side points (any pointer may be NULL): count entries, windows count * 32768 bytes */
 int ppg_index_side_points(const ppg_index *ix, int64_t *bit, int64_t *output, uint8_t *windows);
+/* replaces the index's side points (a host that found inner block starts itself); sorted by output
+ * and bit.  ppg_decompress_chunk splits every chunk at them (ppg_file_decompress_all and ppg_cursor
+ * when a piece or batch is too small to fill the GPU). */
+int ppg_index_set_side_points(ppg_index *ix, int32_t n, const int64_t *bit, const int64_t *output,
+                              const uint8_t *windows);
 
 int ppg_index_build_gpu_file(ppg_ctx *ctx, const char *gz_path, uint32_t chunksize, int64_t piece_bytes,
                              ppg_index **out);
@@ -137,10 +144,17 @@ int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream);
  * [Index[k].Input-1, Index[k+1].Input-1] exactly as LazyFileReader reads them
  * (LazyFileReader.cs:63-69).  out receives to.Output-from.Output bytes; `produced` the count
  * (Core.cs:191).  If recs is non-NULL, up to rec_cap records are written as 4 uint32 newline
- * positions (n1..n4) relative to raw = offset_k ++ out; *nrec gets the record count. */
+ * positions (n1..n4) relative to raw = offset_k ++ out; *nrec gets the record count.
+ * Thread safe (README.md:38-50): concurrent calls on one ctx are combined into shared launches (two
+ * launch slots, each with its own stream and buffers that only grow: no hipMalloc/hipFree per call
+ * once warm); every call gets its own chunk's results.  A chunk of an index with side points
+ * (ppg_index_build_gpu_side) is decoded as one wave per piece. */
 int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
                          uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
                          int64_t *nrec);
+/* ppg_decompress_chunk calls on this ctx so far, the launches that served them, the most calls one
+ * launch served. */
+int ppg_decompress_chunk_stats(ppg_ctx *ctx, int64_t *calls, int64_t *launches, int64_t *max_batch);
 
 /* ======================= DecompressAll over a shard (README "DecompressAll") =======================
  * A shard is chunks [first, first+n) of an index, with their compressed bytes resident on the
@@ -202,6 +216,10 @@ int ppg_shard_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap);
  * entries) on the ctx stream while its output is resident.  NULL / 0 turns it off.  A run with
  * more records than cap fails with PPG_BUF_ERROR. */
 int ppg_shard_set_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap);
+
+/* Whether the last ppg_shard_run of the shard filled the ppg_shard_set_keys buffer (1) or not (0:
+ * none attached, attached after that run, or the run failed). */
+int ppg_shard_keys_ready(ppg_shard *sh);
 
 /* Device-resident per-chunk record counts (int64[n]) copied to caller device memory on this
  * GPU (the input of the cross-GPU all-gather). */
@@ -279,6 +297,13 @@ int ppg_comm_rank(const ppg_comm *c, int32_t *rank, int32_t *nranks);
 void ppg_comm_free(ppg_comm *c);
 int ppg_rccl_version(int *version);    /* ncclGetVersion of the librccl in use */
 
+/* All-to-all-v of int64 values: counts[src * nranks + dst] values go from rank src to rank dst
+ * (the whole matrix, the same on every rank); send holds this rank's outgoing values by
+ * destination, recv receives by source, both in rank order.  RCCL: device buffers on the comm's GPU
+ * (on_device = 1; grouped ncclSend / ncclRecv over xGMI); host transport: host or device buffers,
+ * moved through shared memory in rounds.  The exchange step of ppg_pairs_check. */
+int ppg_comm_alltoallv(ppg_comm *c, const int64_t *send, int64_t *recv, const int64_t *counts, int on_device);
+
 /* bounds[0..nranks]: rank r owns chunks [bounds[r], bounds[r+1]) of [first, first+n) */
 int ppg_partition(const ppg_index *ix, int32_t first, int32_t n, int32_t nranks, int32_t *bounds);
 /* After ppg_shard_run of this rank's shard (chunks [bounds[rank], bounds[rank+1])): the count
@@ -290,6 +315,35 @@ int ppg_shard_gather_counts(ppg_shard *sh, ppg_comm *comm, const int32_t *bounds
  * gather.  counts / bases (may be NULL): Count-1 entries in canonical order. */
 int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, const char *gz_path,
                             int64_t out_capacity, int64_t *counts, int64_t *bases, int64_t *total_records);
+
+/* ============ paired reads: R1 / R2 shards checked record by record ============
+ * The reference only names the goal (README.md:9).  Pair number i = the i-th record of R1 and of
+ * R2 after dropping the records the reference parses twice (key -2); a pair is good when
+ * both spot keys (ppg_shard_keys) are present and equal.  ppg_pairs_check runs on the device: the
+ * shards' keys (their ppg_shard_set_keys buffers when the last run filled them, else extracted now
+ * from one-batch shards), the duplicates dropped through a map, the keys compared.  With a comm
+ * (N ranks; rank r holds R1 and R2 shards of its own contiguous chunk ranges, which do not line up
+ * between the files) pairs are owned evenly by pair number and every key moves to its owner: a
+ * status + count all-gather, one all-to-all-v per file (RCCL ncclSend / ncclRecv, or the host
+ * transport), the compare, a result all-gather; every rank gets the same result and a failing rank
+ * never leaves the others waiting.  Both shards (and an RCCL comm) must be on one GPU.  A ppg_pairs
+ * keeps its device scratch across checks. */
+typedef struct {
+    int64_t pairs;            /* min of the two files' records after dropping duplicates */
+    int64_t records[2];       /* R1 / R2 records after dropping duplicates (all ranks) */
+    int64_t duplicates[2];    /* Q1 duplicates dropped (this rank) */
+    int64_t mismatches;       /* pairs whose keys differ or are missing (< 0), + |records[0] - records[1]| */
+    int64_t first_bad;        /* the first such pair number, or -1 */
+    int64_t first_keys[2];    /* its R1 / R2 spot keys (-1 when a file has no such record) */
+} ppg_pair_result;
+typedef struct ppg_pairs ppg_pairs;
+int ppg_pairs_create(ppg_pairs **out);
+int ppg_pairs_check(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *comm, ppg_pair_result *result);
+/* After a check: the shard record numbers (this rank's shard of `file`, 0 = R1) of pair numbers
+ * [lo, hi), -1 for pairs whose record another rank holds -- record-aligned pair chunks are pair
+ * numbers [j*K, (j+1)*K); the records themselves via ppg_shard_record_base / ppg_shard_copy_records. */
+int ppg_pairs_records(const ppg_pairs *p, int32_t file, int64_t lo, int64_t hi, int64_t *shard_record);
+void ppg_pairs_free(ppg_pairs *p);
 
 /* Library build string (kernel ISA, version). */
 const char *ppg_version(void);

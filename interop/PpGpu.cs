@@ -44,6 +44,17 @@ public unsafe struct PpgBatch          // ppg_batch
     public long* RecOff;                // NChunks + 1
 }
 
+[StructLayout(LayoutKind.Sequential)]
+public unsafe struct PpgPairResult     // ppg_pair_result
+{
+    public long Pairs;
+    public fixed long Records[2];
+    public fixed long Duplicates[2];
+    public long Mismatches;
+    public long FirstBad;
+    public fixed long FirstKeys[2];
+}
+
 internal static unsafe class PpGpu
 {
     const string Lib = "ppgpu";   // libppgpu.so from parallelparsing_amd/
@@ -57,6 +68,8 @@ internal static unsafe class PpGpu
         uint chunksize, long pieceBytes, long outCapacity, long sideBytes, out nint ix);
     [DllImport(Lib)] public static extern int ppg_index_side_count(nint ix);
     [DllImport(Lib)] public static extern int ppg_index_side_points(nint ix, long* bit, long* output, byte* windows);
+    [DllImport(Lib)] public static extern int ppg_index_set_side_points(nint ix, int n, long* bit, long* output,
+        byte* windows);
     [DllImport(Lib)] public static extern int ppg_index_build_gpu_file(nint ctx, string gzPath, uint chunksize,
         long pieceBytes, out nint ix);
     [DllImport(Lib)] public static extern int ppg_index_build_gpu_stats(nint ctx, double* vals, int n);
@@ -84,6 +97,8 @@ internal static unsafe class PpGpu
     // ---- README "Decompress": Core.ExtractDeflateIndex (Core.cs:133-192) + Parsing.Parse ----
     [DllImport(Lib)] public static extern int ppg_decompress_chunk(nint ctx, nint ix, int k, byte* slice,
         long sliceLen, byte* output, long outCap, out long produced, uint* recs, long recCap, out long nrec);
+    [DllImport(Lib)] public static extern int ppg_decompress_chunk_stats(nint ctx, out long calls, out long launches,
+        out long maxBatch);
 
     // ---- README "DecompressAll": a shard of chunks resident on one GPU ----
     [DllImport(Lib)] public static extern int ppg_shard_create(nint ctx, nint ix, int first, int n, byte* comp,
@@ -104,6 +119,7 @@ internal static unsafe class PpGpu
         int dstOnDevice);
     [DllImport(Lib)] public static extern int ppg_shard_keys(nint shard, long* devKeys, long cap);
     [DllImport(Lib)] public static extern int ppg_shard_set_keys(nint shard, long* devKeys, long cap);
+    [DllImport(Lib)] public static extern int ppg_shard_keys_ready(nint shard);
     [DllImport(Lib)] public static extern int ppg_shard_counts_to_device(nint shard, long* devDst);
     [DllImport(Lib)] public static extern int ppg_shard_timing(nint shard, out float inflateMs, out float parseMs,
         out float totalMs);
@@ -128,11 +144,21 @@ internal static unsafe class PpGpu
     [DllImport(Lib)] public static extern int ppg_comm_rank(nint comm, out int rank, out int nranks);
     [DllImport(Lib)] public static extern void ppg_comm_free(nint comm);
     [DllImport(Lib)] public static extern int ppg_rccl_version(out int version);
+    [DllImport(Lib)] public static extern int ppg_comm_alltoallv(nint comm, long* send, long* recv, long* counts,
+        int onDevice);
     [DllImport(Lib)] public static extern int ppg_partition(nint ix, int first, int n, int nranks, int* bounds);
     [DllImport(Lib)] public static extern int ppg_shard_gather_counts(nint shard, nint comm, int* bounds,
         long* counts, long* bases, out long totalRecords);
     [DllImport(Lib)] public static extern int ppg_dist_decompress_all(nint ctx, nint comm, nint ix, string gzPath,
         long outCapacity, long* counts, long* bases, out long totalRecords);
+
+    // ---- paired reads (SURVEY §8f #3, README.md:9): R1 / R2 shards checked on the device ----
+    [DllImport(Lib)] public static extern int ppg_pairs_create(out nint pairs);
+    [DllImport(Lib)] public static extern int ppg_pairs_check(nint pairs, nint r1, nint r2, nint comm,
+        out PpgPairResult result);
+    [DllImport(Lib)] public static extern int ppg_pairs_records(nint pairs, int file, long lo, long hi,
+        long* shardRecord);
+    [DllImport(Lib)] public static extern void ppg_pairs_free(nint pairs);
 
     [DllImport(Lib)] public static extern nint ppg_version();
     [DllImport(Lib)] public static extern nint ppg_build_id();

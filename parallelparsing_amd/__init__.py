@@ -105,6 +105,16 @@ class Index:
             return np.zeros(0, np.uint8)
         return np.frombuffer(C.string_at(lib.ppg_index_window(self._h, 0), n * WINSIZE), np.uint8)
 
+    def set_side_points(self, bits, outputs, windows):
+        """Attach side points (inner deflate block starts: absolute bit, output offset, the 32 KiB
+        before each) found by the host, as BuildDeflateIndexGpu(side_bytes=...) records them
+        (ppg_index_set_side_points)."""
+        b, o = np.ascontiguousarray(bits, np.int64), np.ascontiguousarray(outputs, np.int64)
+        w = np.ascontiguousarray(windows, np.uint8)
+        assert w.size == 32768 * b.size and o.size == b.size
+        check(lib.ppg_index_set_side_points(self._h, b.size, _ptr(b), _ptr(o), _ptr(w)), "ppg_index_set_side_points")
+        return self
+
     def side_points(self, first=0, n=None):
         """(bits, outputs, windows) of the side points BuildDeflateIndexGpu(side_bytes=...) recorded,
         those inside chunks [first, first+n) (a Shard's range) -- Shard.set_split's arguments."""
@@ -181,6 +191,13 @@ class Device:
     def stream_wait(self, stream):
         """Order `stream`'s later work after everything queued on this ctx so far (ppg_stream_wait_ctx)."""
         check(lib.ppg_stream_wait_ctx(self._h, C.c_void_p(_stream_handle(stream))), "ppg_stream_wait_ctx")
+
+    def decompress_chunk_stats(self):
+        """{calls, launches, max_batch} of ppg_decompress_chunk on this ctx: how the thread-safe
+        per-chunk Decompress combined concurrent calls into launches."""
+        v = [C.c_int64() for _ in range(3)]
+        check(lib.ppg_decompress_chunk_stats(self._h, *[C.byref(x) for x in v]), "ppg_decompress_chunk_stats")
+        return dict(zip(("calls", "launches", "max_batch"), (x.value for x in v)))
 
     def after_torch(self):
         """wait_stream(torch's current stream on this device): call before a ppg call reads device
@@ -335,7 +352,9 @@ class Core:
     def ExtractDeflateIndex(file_buffer, index, k, buf=None, device=None, with_records=False):
         """Decompress checkpoint k (Core.cs:133-192) on the GPU.  file_buffer = file bytes
         [Index[k].Input-1, Index[k+1].Input-1].  Returns the produced byte count written into buf
-        (allocated if None) — and the (n,4) record descriptors if with_records."""
+        (allocated if None) — and the (n,4) record descriptors if with_records.  Thread safe, as
+        README.md:38-50 requires: concurrent calls on one Device share launches
+        (ppg_decompress_chunk; ctypes releases the GIL for the call)."""
         dev = device or Device.default()
         src = _as_u8(file_buffer)
         o0, _, _, _ = index.point_fields(k)
@@ -526,6 +545,20 @@ class Comm:
     @property
     def handle(self):
         return self._h
+
+    def alltoallv(self, send, counts):
+        """ppg_comm_alltoallv over host memory (the host transport): counts[src, dst] int64 values go
+        from rank src to rank dst; `send` holds this rank's by destination.  Returns what this rank
+        receives, by source."""
+        c = np.ascontiguousarray(counts, np.int64)
+        r, n = self.rank_size()
+        assert c.shape == (n, n)
+        snd = np.ascontiguousarray(send, np.int64)
+        assert snd.size == c[r].sum()
+        rcv = np.zeros(max(1, int(c[:, r].sum())), np.int64)
+        check(lib.ppg_comm_alltoallv(self._h, _ptr(snd if snd.size else np.zeros(1, np.int64)), _ptr(rcv), _ptr(c), 0),
+              "ppg_comm_alltoallv")
+        return rcv[:int(c[:, r].sum())]
 
     def rank_size(self):
         r, n = C.c_int32(), C.c_int32()

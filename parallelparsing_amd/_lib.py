@@ -69,6 +69,7 @@ _SIGS = {
     "ppg_index_build_gpu": (C.c_int, [vp, vp, i64, C.c_int, u32, i64, i64, P(vp)]),
     "ppg_index_build_gpu_side": (C.c_int, [vp, vp, i64, C.c_int, u32, i64, i64, i64, P(vp)]),
     "ppg_index_side_count": (C.c_int, [vp]),
+    "ppg_index_set_side_points": (C.c_int, [vp, i32, vp, vp, vp]),
     "ppg_index_side_points": (C.c_int, [vp, vp, vp, vp]),
     "ppg_index_build_gpu_file": (C.c_int, [vp, C.c_char_p, u32, i64, P(vp)]),
     "ppg_index_build_gpu_stats": (C.c_int, [vp, P(C.c_double), i32]),
@@ -89,6 +90,7 @@ _SIGS = {
     "ppg_ctx_wait_stream": (C.c_int, [vp, vp]),
     "ppg_stream_wait_ctx": (C.c_int, [vp, vp]),
     "ppg_decompress_chunk": (C.c_int, [vp, vp, i32, vp, i64, vp, i64, P(i64), vp, i64, P(i64)]),
+    "ppg_decompress_chunk_stats": (C.c_int, [vp, P(i64), P(i64), P(i64)]),
     "ppg_shard_create": (C.c_int, [vp, vp, i32, i32, vp, i64, C.c_int, i64, P(vp)]),
     "ppg_shard_free": (None, [vp]),
     "ppg_shard_run": (C.c_int, [vp]),
@@ -121,6 +123,12 @@ _SIGS = {
     "ppg_partition": (C.c_int, [vp, i32, i32, i32, vp]),
     "ppg_shard_gather_counts": (C.c_int, [vp, vp, vp, vp, vp, P(i64)]),
     "ppg_dist_decompress_all": (C.c_int, [vp, vp, vp, C.c_char_p, i64, vp, vp, P(i64)]),
+    "ppg_shard_keys_ready": (C.c_int, [vp]),
+    "ppg_comm_alltoallv": (C.c_int, [vp, vp, vp, vp, C.c_int]),
+    "ppg_pairs_create": (C.c_int, [P(vp)]),
+    "ppg_pairs_check": (C.c_int, [vp, vp, vp, vp, vp]),
+    "ppg_pairs_records": (C.c_int, [vp, i32, i64, i64, vp]),
+    "ppg_pairs_free": (None, [vp]),
 }
 
 
@@ -129,6 +137,14 @@ class PpgBatch(C.Structure):
     _fields_ = [("first_chunk", C.c_int32), ("nchunks", C.c_int32), ("record_base", C.c_int64),
                 ("nrecords", C.c_int64), ("text", C.c_void_p), ("raw_off", C.POINTER(C.c_int64)),
                 ("desc", C.POINTER(C.c_uint32)), ("rec_off", C.POINTER(C.c_int64))]
+
+
+class PpgPairResult(C.Structure):
+    """ppg_pair_result (include/ppgpu.h)."""
+    _fields_ = [("pairs", C.c_int64), ("records", C.c_int64 * 2), ("duplicates", C.c_int64 * 2),
+                ("mismatches", C.c_int64), ("first_bad", C.c_int64), ("first_keys", C.c_int64 * 2)]
+
+
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
     _f.restype = _res

@@ -353,6 +353,7 @@ int ppg_open(int device, ppg_ctx **out) {
     auto ctx = std::make_unique<ppg_ctx>();
     ctx->device = device;
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    ctx->chunks = chunk_service_new();
     if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(10, atoi(rb)));
     if (const char *lb = getenv("PPG_LIT_BITS")) ctx->lit_bits = std::min(9, std::max(8, atoi(lb)));
     if (ppg_inflate_lds_bytes(ctx->ring_bits, ctx->lit_bits) == 0) { ctx->ring_bits = 10; ctx->lit_bits = 8; }
@@ -368,6 +369,7 @@ void ppg_close(ppg_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     ingest_free(ctx->ingest);
+    chunk_service_free(ctx->chunks);
     if (ctx->stage) (void)hipHostFree(ctx->stage);
     if (ctx->handoff) (void)hipEventDestroy(ctx->handoff);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -424,12 +426,33 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
     if (base_byte < 0) return PPG_ARG_ERROR;
     if (const int v = ppg_index_validate(ix, first, n); v != PPG_OK) return v;
     if (comp_len != P[(size_t)first + n].input - P[(size_t)first].input + 1) return PPG_ARG_ERROR;
-    if (((uintptr_t)comp & 3) != 0) return PPG_ARG_ERROR;
+    if (ix->windows.size() < ((size_t)first + n) * kWin) return PPG_ARG_ERROR;
+    std::vector<ChunkSpec> spec((size_t)n);
+    for (int32_t i = 0; i < n; i++)
+        spec[(size_t)i] = ChunkSpec{&P[(size_t)first + i], &P[(size_t)first + i + 1], ix->win((size_t)first + i),
+                                    P[(size_t)first + i].input - 1 - base_byte, (size_t)first + i + 2 == P.size()};
+    const int rc = shard_prepare_specs(sh, spec.data(), n, comp, comp_len, out_capacity, s,
+                                       n ? ix->win((size_t)first) : nullptr);
+    if (rc != PPG_OK) return rc;
+    // the chunks are one contiguous range of the file: absolute coordinates (ppg_shard_set_split
+    // takes side points in file bits and stream output offsets)
     sh->first = first;
-    sh->n = n;
     sh->base_byte = base_byte;
-    sh->h_pout.resize((size_t)n + 1);
     for (int32_t i = 0; i <= n; i++) sh->h_pout[(size_t)i] = P[(size_t)first + i].output;
+    return PPG_OK;
+}
+
+// The same for any list of chunks, each with its own place in comp (ppg_decompress_chunk gathers
+// the slices of unrelated chunks, possibly of different indexes, into one launch).  Coordinates are
+// virtual: base_byte 0, h_pout[k] = the chunk's output offset in the (single-batch, when
+// out_capacity = 0) output buffer; windows_contig, when non-null, holds the n windows back to back.
+int shard_prepare_specs(ppg_shard *sh, const ChunkSpec *spec, int32_t n, const uint8_t *comp, int64_t comp_len,
+                        int64_t out_capacity, hipStream_t s, const uint8_t *windows_contig) {
+    if (((uintptr_t)comp & 3) != 0) return PPG_ARG_ERROR;
+    sh->first = 0;
+    sh->n = n;
+    sh->base_byte = 0;
+    sh->h_pout.resize((size_t)n + 1);
     sh->nsub = 0;
     sh->comp = comp;
     sh->comp_len = comp_len;
@@ -437,8 +460,8 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
     sh->ran = 0;
     sh->batches.clear();
     // batches: consecutive chunks whose outputs fit out_capacity (0 = everything at once)
-    int64_t total_out = P[(size_t)first + n].output - P[(size_t)first].output;
-    if (total_out < 0) return PPG_ARG_ERROR;
+    int64_t total_out = 0;
+    for (int32_t i = 0; i < n; i++) total_out += std::max<int64_t>(spec[i].to->output - spec[i].from->output, 0);
     int64_t cap = out_capacity > 0 ? out_capacity : total_out;
     sh->h_jobs.resize((size_t)n);
     int64_t need_max = 0;
@@ -449,49 +472,52 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
     if (const char *e = getenv("PPG_NL_BYTES")) nl_bytes = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     {
         int32_t b0 = 0;
-        int64_t bbase = P[(size_t)first].output;
+        int64_t pos = 0, bbase = 0;   // output offset of chunk i in the whole list / of its batch
         for (int32_t i = 0; i < n; i++) {
-            const PpgPoint &from = P[(size_t)first + i], &to = P[(size_t)first + i + 1];
+            const PpgPoint &from = *spec[i].from, &to = *spec[i].to;
             int64_t ulen = to.output - from.output;
             if (ulen < 0) ulen = 0;   // Core.cs:145: len < 0 -> nothing produced
-            if (to.output - bbase > cap && i > b0) {
+            if (pos + ulen - bbase > cap && i > b0) {
                 sh->batches.push_back({b0, i});
-                need_max = std::max(need_max, from.output - bbase);
+                need_max = std::max(need_max, pos - bbase);
                 b0 = i;
-                bbase = from.output;
+                bbase = pos;
             }
+            sh->h_pout[(size_t)i] = pos;
             PpgInflateJob &J = sh->h_jobs[(size_t)i];
-            J.bit_start = (uint64_t)(8 * (from.input - base_byte) - from.bits);
-            J.bit_limit = (uint64_t)(8 * (to.input - base_byte));
-            J.out_off = (uint64_t)(from.output - bbase);
+            const int64_t cb = spec[i].comp_byte;   // comp offset of file byte from.Input - 1
+            J.bit_start = (uint64_t)(8 * (cb + 1) - from.bits);
+            J.bit_limit = (uint64_t)(8 * (cb + 1 + to.input - from.input));
+            J.out_off = (uint64_t)(pos - bbase);
             J.out_len = (uint64_t)ulen;
             J.dict_off = (uint64_t)i * kWin;
-            J.expect_end = (size_t)first + i + 2 == P.size() ? ~0ull : (uint64_t)(8 * (to.input - base_byte) - to.bits);
+            J.expect_end = spec[i].last ? ~0ull : (uint64_t)(8 * (cb + 1 + to.input - from.input) - to.bits);
             // newline census (offsets relative to the batch, like out_off)
             if (i == b0) nl_batch = 0;
-            const uint64_t cap = nl_bytes >= (1ull << 40) ? 0 : (uint64_t)ulen / nl_bytes + 64;
+            const uint64_t ncap = nl_bytes >= (1ull << 40) ? 0 : (uint64_t)ulen / nl_bytes + 64;
             J.nl_off = nl_batch;
-            J.nl_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFFFu);
+            J.nl_cap = (uint32_t)std::min<uint64_t>(ncap, 0xFFFFFFFFu);
             nl_batch += J.nl_cap;
             nl_need = std::max(nl_need, nl_batch);
             J.raw_shift = (uint32_t)from.offset.size();
             J.prev_byte = from.offset.empty() ? (uint32_t)'\n' : (uint32_t)from.offset.back();
             J.pad = 0;
+            pos += ulen;
         }
+        sh->h_pout[(size_t)n] = pos;
         if (n > 0) {
             sh->batches.push_back({b0, n});
-            need_max = std::max(need_max, P[(size_t)first + n].output - bbase);
+            need_max = std::max(need_max, pos - bbase);
         }
     }
     const int64_t out_cap = std::max<int64_t>(need_max, 0);
     HIPCHK(sh->jobs.alloc((size_t)n));
     HIPCHK(hipMemcpyAsync(sh->jobs.p, sh->h_jobs.data(), sizeof(PpgInflateJob) * (size_t)n, hipMemcpyHostToDevice, s));
-    // windows (contiguous in the index) and offsets of the shard's `from` points
-    if (ix->windows.size() < ((size_t)first + n) * kWin) return PPG_ARG_ERROR;
+    // windows and offsets of the chunks' `from` points
     std::vector<PpgOffsetRef> horef((size_t)n);
     std::vector<uint8_t> hoff;
     for (int32_t i = 0; i < n; i++) {
-        const PpgPoint &from = P[(size_t)first + i];
+        const PpgPoint &from = *spec[i].from;
         horef[(size_t)i].start = hoff.size();
         horef[(size_t)i].len = (uint32_t)from.offset.size();
         // the offset's own newlines, and whether it alone breaks R-P3 (raw[0] == '\n', "\n\n", NUL)
@@ -509,7 +535,13 @@ int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, 
         hoff.insert(hoff.end(), from.offset.begin(), from.offset.end());
     }
     HIPCHK(sh->dicts.alloc((size_t)n * kWin));
-    HIPCHK(hipMemcpyAsync(sh->dicts.p, ix->win((size_t)first), (size_t)n * kWin, hipMemcpyHostToDevice, s));
+    ByteVec hwin;
+    if (!windows_contig && n) {   // scattered windows: one staging copy, one H2D
+        hwin.resize((size_t)n * kWin);
+        for (int32_t i = 0; i < n; i++) memcpy(hwin.data() + (size_t)i * kWin, spec[i].window, kWin);
+        windows_contig = hwin.data();
+    }
+    if (n) HIPCHK(hipMemcpyAsync(sh->dicts.p, windows_contig, (size_t)n * kWin, hipMemcpyHostToDevice, s));
     HIPCHK(sh->offs.alloc(hoff.size() + 16));
     if (!hoff.empty()) HIPCHK(hipMemcpyAsync(sh->offs.p, hoff.data(), hoff.size(), hipMemcpyHostToDevice, s));
     HIPCHK(sh->oref.alloc((size_t)n));
@@ -730,7 +762,9 @@ static int shard_run(ppg_shard *sh) {
 
 int ppg_shard_run(ppg_shard *sh) {
     if (!sh) return PPG_ARG_ERROR;
+    sh->keys_written = 0;
     sh->last_rc = shard_run(sh);
+    sh->keys_written = sh->last_rc == PPG_OK && sh->keys_dev != nullptr;
     return sh->last_rc;
 }
 
@@ -887,8 +921,11 @@ int ppg_shard_set_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap) {
     if (!sh || cap < 0 || (dev_keys == nullptr) != (cap == 0)) return PPG_ARG_ERROR;
     sh->keys_dev = dev_keys;
     sh->keys_cap = cap;
+    sh->keys_written = 0;   // filled by the next run, not by an earlier one
     return PPG_OK;
 }
+
+int ppg_shard_keys_ready(ppg_shard *sh) { return sh && sh->keys_written ? 1 : 0; }
 
 int ppg_shard_keys(ppg_shard *sh, int64_t *dev_keys, int64_t cap) {
     if (!sh || !sh->ran || sh->batches.size() != 1 || !dev_keys) return PPG_ARG_ERROR;
@@ -939,25 +976,7 @@ int ppg_shard_timing(ppg_shard *sh, float *inflate_ms, float *parse_ms, float *t
     return PPG_OK;
 }
 
-// README "Decompress": one checkpoint from a host slice, through a one-chunk shard.
-int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
-                         uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
-                         int64_t *nrec) {
-    if (!ctx || !ix || !slice || k < 0 || (size_t)k + 1 >= ix->pts.size()) return PPG_ARG_ERROR;
-    ppg_shard *sh = nullptr;
-    int rc = ppg_shard_create(ctx, ix, k, 1, slice, slice_len, 0, 0, &sh);
-    if (rc != PPG_OK) return rc;
-    rc = ppg_shard_run(sh);
-    if (rc == PPG_OK) {
-        int64_t len = 0;
-        if (out) rc = ppg_shard_copy_chunk(sh, 0, out, out_cap, &len);
-        else len = (int64_t)sh->h_res[0].produced;
-        if (produced) *produced = len;
-        if (rc == PPG_OK) rc = ppg_shard_copy_records(sh, 0, recs, rec_cap, nrec);
-    }
-    ppg_shard_free(sh);
-    return rc;
-}
+// README "Decompress" (ppg_decompress_chunk): ppg_chunk.cpp
 
 }  // extern "C"
 

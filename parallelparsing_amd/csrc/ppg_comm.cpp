@@ -37,6 +37,11 @@ struct Rccl {
     ncclResult_t (*destroy)(ncclComm_t) = nullptr;
     const char *(*err)(ncclResult_t) = nullptr;
     ncclResult_t (*version)(int *) = nullptr;
+    // point-to-point (the paired-read key exchange, ppg_pairs.hip); optional
+    ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
     bool load() {
         if (h) return true;
         // the copy already in the process (torch's), else the ROCm one
@@ -51,6 +56,10 @@ struct Rccl {
         destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
         err = (decltype(err))dlsym(h, "ncclGetErrorString");
         version = (decltype(version))dlsym(h, "ncclGetVersion");
+        send = (decltype(send))dlsym(h, "ncclSend");
+        recv = (decltype(recv))dlsym(h, "ncclRecv");
+        group_start = (decltype(group_start))dlsym(h, "ncclGroupStart");
+        group_end = (decltype(group_end))dlsym(h, "ncclGroupEnd");
         return get_unique_id && init_rank && all_gather && destroy && err;
     }
 };
@@ -84,6 +93,7 @@ static_assert(sizeof(ShmHdr) <= 64, "header fits the segment's first 64 bytes");
 constexpr uint64_t kShmMagic = 0x7070677368636F6Dull;   // "ppgshcom"
 constexpr int64_t kShmSlot = 8 << 20;   // bytes per rank per all-gather (1M chunk counts)
 constexpr int kShmTimeoutS = 300;
+constexpr size_t kStatSlots = 8;        // int64 per rank in the buffer made with an RCCL comm (status gathers)
 
 }  // namespace
 
@@ -154,7 +164,7 @@ struct ppg_comm {
     int rccl_setup() {
         HIPCHK(hipSetDevice(device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        HIPCHK(stat.alloc(2 * ((size_t)nranks + 1)));
+        HIPCHK(stat.alloc(kStatSlots * ((size_t)nranks + 1)));
         return PPG_OK;
     }
 };
@@ -437,3 +447,95 @@ int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, c
 }
 
 }  // extern "C"
+
+// ---- collectives for the other multi-rank steps of the library (ppg_pairs.hip) ----
+
+int comm_size(const ppg_comm *c, int32_t *rank, int32_t *nranks) { return ppg_comm_rank(c, rank, nranks); }
+int comm_device(const ppg_comm *c) { return c->host() ? -1 : c->device; }
+
+// All-gather of n <= 8 int64 per rank (statuses and counts), host memory in and out, over either
+// transport, from a buffer made with the comm (nothing to allocate, so every rank always joins).
+// sent_ok reports a failed copy into the collective (the others then got stale data).
+int comm_all_gather_i64(ppg_comm *c, const int64_t *send, int64_t *recv, size_t n, bool &sent_ok) {
+    sent_ok = true;
+    if (c->host()) return c->host_all_gather(send, recv, 8 * (int64_t)n);
+    if (n > kStatSlots) return PPG_UNSUPPORTED;   // status-sized gathers only: the buffer exists already
+    HIPCHK(hipSetDevice(c->device));
+    return c->rccl_all_gather(c->stat, send, recv, n, sent_ok);
+}
+
+// All-to-all-v of int64 between device buffers on this rank's GPU.  m = the R x R count matrix
+// (m[src * R + dst] elements), known to every rank; send / recv are laid out by destination /
+// source in rank order.  RCCL: grouped ncclSend / ncclRecv on the comm's stream (xGMI
+// point-to-point); host transport: staged through host memory in rounds of the shared slots.
+// The caller's stream s must have produced `send` (it is synchronised first).  Every rank runs
+// every round whatever its own errors (the others would wait); the first error is returned after.
+int comm_alltoallv_i64(ppg_comm *c, hipStream_t s, const int64_t *send, int64_t *recv, const int64_t *m,
+                       bool on_device) {
+    const int32_t R = c->nranks, me = c->rank;
+    std::vector<int64_t> sd((size_t)R + 1, 0), rd((size_t)R + 1, 0);
+    for (int32_t q = 0; q < R; q++) {
+        sd[(size_t)q + 1] = sd[(size_t)q] + m[(size_t)me * R + q];
+        rd[(size_t)q + 1] = rd[(size_t)q] + m[(size_t)q * R + me];
+    }
+    int rc = !s || hipStreamSynchronize(s) == hipSuccess ? PPG_OK : PPG_DEVICE_ERROR;
+    if (!c->host()) {
+        if (!on_device) return PPG_ARG_ERROR;   // RCCL moves device memory only
+        if (!rccl().send || !rccl().recv || !rccl().group_start || !rccl().group_end) return PPG_UNSUPPORTED;
+        HIPCHK(hipSetDevice(c->device));
+        RCCLCHK(rccl().group_start());
+        for (int32_t q = 0; q < R; q++) {
+            if (q == me) continue;
+            if (m[(size_t)me * R + q])
+                RCCLCHK(rccl().send(send + sd[(size_t)q], (size_t)m[(size_t)me * R + q], ncclInt64, q, c->nccl, c->stream));
+            if (m[(size_t)q * R + me])
+                RCCLCHK(rccl().recv(recv + rd[(size_t)q], (size_t)m[(size_t)q * R + me], ncclInt64, q, c->nccl, c->stream));
+        }
+        RCCLCHK(rccl().group_end());
+        if (m[(size_t)me * R + me])
+            HIPCHK(hipMemcpyAsync(recv + rd[(size_t)me], send + sd[(size_t)me], 8 * (size_t)m[(size_t)me * R + me],
+                                  hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return rc;
+    }
+    // host transport: this rank's outgoing keys to host memory, rounds through the slots, back
+    std::vector<int64_t> hs, hr;
+    const int64_t *src_all = send;
+    int64_t *dst_all = recv;
+    if (on_device) {
+        hs.resize((size_t)sd[(size_t)R]);
+        hr.resize((size_t)rd[(size_t)R]);
+        if (rc == PPG_OK && !hs.empty() && hipMemcpy(hs.data(), send, 8 * hs.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = PPG_DEVICE_ERROR;
+        src_all = hs.data();
+        dst_all = hr.data();
+    }
+    const int64_t quota = kShmSlot / 8 / R;   // elements per (src, dst) per round
+    int64_t maxc = 0;
+    for (int64_t i = 0; i < (int64_t)R * R; i++) maxc = std::max(maxc, m[i]);
+    const int64_t rounds = (maxc + quota - 1) / quota;
+    for (int64_t t = 0; t < rounds; t++) {
+        int64_t *mine = (int64_t *)(c->slots + (size_t)me * kShmSlot);
+        for (int32_t q = 0; q < R; q++) {
+            const int64_t n = std::min(quota, std::max<int64_t>(0, m[(size_t)me * R + q] - t * quota));
+            if (n) memcpy(mine + (size_t)q * quota, src_all + sd[(size_t)q] + t * quota, 8 * (size_t)n);
+        }
+        if (int b = c->barrier()) return b;
+        for (int32_t q = 0; q < R; q++) {
+            const int64_t n = std::min(quota, std::max<int64_t>(0, m[(size_t)q * R + me] - t * quota));
+            const int64_t *src = (const int64_t *)(c->slots + (size_t)q * kShmSlot) + (size_t)me * quota;
+            if (n) memcpy(dst_all + rd[(size_t)q] + t * quota, src, 8 * (size_t)n);
+        }
+        if (int b = c->barrier()) return b;
+    }
+    if (on_device && rc == PPG_OK && !hr.empty() &&
+        hipMemcpy(recv, hr.data(), 8 * hr.size(), hipMemcpyHostToDevice) != hipSuccess)
+        rc = PPG_DEVICE_ERROR;
+    return rc;
+}
+
+extern "C" int ppg_comm_alltoallv(ppg_comm *c, const int64_t *send, int64_t *recv, const int64_t *counts,
+                                  int on_device) {
+    if (!c || !counts) return PPG_ARG_ERROR;
+    return comm_alltoallv_i64(c, nullptr, send, recv, counts, on_device != 0);
+}

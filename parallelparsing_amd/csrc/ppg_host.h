@@ -94,6 +94,9 @@ struct ppg_index {
 };
 
 struct IngestState;   // host-ingest buffers kept across ppg_file_decompress_all calls
+struct ChunkService;  // ppg_decompress_chunk's launch slots and request queue (ppg_chunk.cpp)
+ChunkService *chunk_service_new();
+void chunk_service_free(ChunkService *svc);
 
 constexpr int kIxStats = 18;   // ppg_index_build_gpu_stats values (parallelparsing_amd.Core.GPU_INDEX_STATS)
 
@@ -102,6 +105,7 @@ struct ppg_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t handoff = nullptr;   // ppg_ctx_wait_stream / ppg_stream_wait_ctx
     IngestState *ingest = nullptr;
+    ChunkService *chunks = nullptr;
     int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
     int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)
     double ix_stats[kIxStats] = {0};   // timings / counts of the last GPU CreateIndex (ppg_index_build_gpu_stats)
@@ -177,6 +181,7 @@ struct ppg_shard {
     // ppg_shard_set_keys: every batch also writes its records' spot keys here (global record number)
     int64_t *keys_dev = nullptr;
     int64_t keys_cap = 0;
+    int keys_written = 0;   // the last successful run filled keys_dev (set by shard_run)
     // split chunks (ppg_shard_set_split): the inflate launch runs sub-jobs, ppg_split_merge folds
     // them back into per-chunk results and census regions
     int32_t nsub = 0;                            // side points in use (0: one wave per chunk)
@@ -189,6 +194,15 @@ struct ppg_shard {
     std::vector<uint32_t> h_sidx;
 };
 
+// one chunk of a shard: its Points, its window and where file byte from.Input-1 sits in comp
+struct ChunkSpec {
+    const PpgPoint *from, *to;
+    const uint8_t *window;
+    int64_t comp_byte;
+    bool last;                          // `to` is the index's final Point (R-E5 end not checkable)
+};
+int shard_prepare_specs(ppg_shard *sh, const ChunkSpec *spec, int32_t n, const uint8_t *comp, int64_t comp_len,
+                        int64_t out_capacity, hipStream_t s, const uint8_t *windows_contig);
 int shard_prepare(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n, const uint8_t *comp, int64_t comp_len,
                   int64_t out_capacity, hipStream_t s);
 hipStream_t shard_stream(const ppg_shard *sh);
@@ -200,3 +214,10 @@ int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, in
 int shard_reserve(ppg_shard *sh, const ppg_index *ix, int32_t first,
                   const std::vector<std::pair<int32_t, int32_t>> &ranges, bool split);
 bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads);
+
+// collectives of a ppg_comm beyond the count gather (ppg_comm.cpp), used by ppg_pairs.hip
+int comm_size(const ppg_comm *c, int32_t *rank, int32_t *nranks);
+int comm_device(const ppg_comm *c);   // -1: host transport
+int comm_all_gather_i64(ppg_comm *c, const int64_t *send, int64_t *recv, size_t n, bool &sent_ok);
+int comm_alltoallv_i64(ppg_comm *c, hipStream_t s, const int64_t *send, int64_t *recv, const int64_t *m,
+                       bool on_device);

@@ -917,6 +917,18 @@ int ppg_index_side_points(const ppg_index *ix, int64_t *bit, int64_t *output, ui
     return PPG_OK;
 }
 
+int ppg_index_set_side_points(ppg_index *ix, int32_t n, const int64_t *bit, const int64_t *output,
+                              const uint8_t *windows) {
+    if (!ix || n < 0 || (n && (!bit || !output || !windows))) return PPG_ARG_ERROR;
+    for (int32_t i = 1; i < n; i++)
+        if (output[i] <= output[i - 1] || bit[i] <= bit[i - 1]) return PPG_ARG_ERROR;
+    ix->side_bit.assign(bit, bit + n);
+    ix->side_out.assign(output, output + n);
+    ix->side_win.resize((size_t)n * kWin);
+    if (n) memcpy(ix->side_win.data(), windows, (size_t)n * kWin);
+    return PPG_OK;
+}
+
 int ppg_index_build_gpu_side(ppg_ctx *ctx, const void *gz, int64_t gz_len, int gz_on_device, uint32_t chunksize,
                              int64_t piece_bytes, int64_t out_capacity, int64_t side_bytes, ppg_index **out) {
     if (!ctx || !gz || gz_len <= 0 || !out) return PPG_ARG_ERROR;

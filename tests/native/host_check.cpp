@@ -13,6 +13,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <string>
 #include <thread>
@@ -132,6 +133,46 @@ static void check_comm(const std::string &gz_path, uint32_t chunk, int world, in
     ppg_index_free(ix);
 }
 
+// ppg_comm_alltoallv over the host transport with `world` ranks as threads, host buffers: uneven
+// and zero counts and one pair large enough for several rounds of the shared slots; then
+// ppg_pairs_check with no shards on every rank (every rank joins the status gather and fails alike)
+static void check_alltoallv(int world) {
+    char name[64];
+    snprintf(name, sizeof name, "/ppg_hc_a2a_%d_%d", (int)getpid(), world);
+    std::vector<int64_t> m((size_t)world * world);
+    for (int a = 0; a < world; a++)
+        for (int b = 0; b < world; b++) m[(size_t)a * world + b] = (a * 7 + b * 13) % 11 * 97;
+    m[(size_t)world - 1] = 1500000;   // rank 0 -> last rank: several rounds
+    m[(size_t)(world - 1) * world] = 0;
+    std::vector<std::thread> th;
+    std::atomic<int> ok{0};
+    for (int r = 0; r < world; r++) {
+        th.emplace_back([&, r] {
+            ppg_comm *c = nullptr;
+            if (ppg_comm_init_host(world, r, name, &c) != PPG_OK) return;
+            std::vector<int64_t> send, want;
+            for (int d = 0; d < world; d++)
+                for (int64_t i = 0; i < m[(size_t)r * world + d]; i++) send.push_back(r * 10000000LL + d * 1000000LL + i);
+            for (int s2 = 0; s2 < world; s2++)
+                for (int64_t i = 0; i < m[(size_t)s2 * world + r]; i++) want.push_back(s2 * 10000000LL + r * 1000000LL + i);
+            std::vector<int64_t> recv(want.size() + 1, -7);
+            int64_t dummy = 0;
+            const int rc = ppg_comm_alltoallv(c, send.empty() ? &dummy : send.data(), recv.data(), m.data(), 0);
+            CHECK(rc == PPG_OK);
+            CHECK(std::equal(want.begin(), want.end(), recv.begin()));
+            ppg_pairs *p = nullptr;
+            CHECK(ppg_pairs_create(&p) == PPG_OK);
+            ppg_pair_result res;
+            CHECK(ppg_pairs_check(p, nullptr, nullptr, c, &res) == PPG_ARG_ERROR);
+            ppg_pairs_free(p);
+            ppg_comm_free(c);
+            ok++;
+        });
+    }
+    for (auto &t : th) t.join();
+    CHECK(ok == world);
+}
+
 int main(int argc, char **argv) {
     if (argc < 3) {
         fprintf(stderr, "usage: host_check <golden dir> <scratch dir>\n");
@@ -152,6 +193,7 @@ int main(int argc, char **argv) {
         for (auto &t : th) t.join();
     }
     for (int world : {2, 3, 5}) check_comm(g + "/l6_c200.gz", 200, world, 4);
+    for (int world : {2, 3}) check_alltoallv(world);
     printf("host_check: %s (%d failures)\n", failures ? "FAILED" : "ok", failures.load());
     return failures ? 1 : 0;
 }

@@ -192,3 +192,79 @@ def test_rank_enumerators_cover_the_file_in_order(world):
     assert nxt == m
     with pytest.raises(ValueError):
         pp.BatchedFASTQ(ix, "unused.gz", rank=world, world=world)
+
+
+def _a2a_rank(rank, world, name, counts, q):
+    import numpy as _np
+    import parallelparsing_amd as pp
+    try:
+        c = pp.Comm.host(world, rank, name)
+        # rank r sends to rank d the values r * 10**7 + d * 10**6 + i, i < counts[r, d]
+        send = _np.concatenate([rank * 10**7 + d * 10**6 + _np.arange(counts[rank, d], dtype=_np.int64)
+                                for d in range(world)])
+        got = c.alltoallv(send, counts)
+        c.close()
+        q.put((rank, got.tolist()))
+    except Exception as e:   # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_alltoallv_in_rounds(world):
+    """ppg_comm_alltoallv over the host transport (the paired-read key exchange's collective,
+    ppg_pairs_check, rehearsed on a one-GPU box): uneven counts, zero counts and counts larger than
+    one round of the shared slots (8 MiB per rank) arrive complete and in source order.  No GPU."""
+    import uuid
+    import torch.multiprocessing as mp
+    rng = np.random.default_rng(world)
+    counts = rng.integers(0, 3000, (world, world)).astype(np.int64)
+    counts[0, world - 1] = 1_300_000   # several rounds
+    counts[world - 1, 0] = 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/ppg_cpu_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_a2a_rank, args=(r, world, name, counts, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+    for r in range(world):
+        exp = np.concatenate([s * 10**7 + r * 10**6 + np.arange(counts[s, r], dtype=np.int64) for s in range(world)])
+        assert res[r] == exp.tolist(), (r, str(res[r])[:200])
+
+
+def _pairs_no_device(rank, world, name, q):
+    import parallelparsing_amd as pp
+    from parallelparsing_amd._lib import lib, PpgPairResult
+    import ctypes as C
+    try:
+        c = pp.Comm.host(world, rank, name)
+        h = C.c_void_p()
+        assert lib.ppg_pairs_create(C.byref(h)) == 0
+        res = PpgPairResult()
+        # no shards on any rank (no GPU here): every rank joins the status gather and fails alike
+        rc = lib.ppg_pairs_check(h, None, None, c.handle, C.byref(res))
+        lib.ppg_pairs_free(h)
+        c.close()
+        q.put((rank, rc))
+    except Exception as e:   # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e)))
+
+
+def test_pairs_check_failing_ranks_meet():
+    """ppg_pairs_check on two ranks with nothing to check: both join the status gather and return
+    the same PPG_ARG_ERROR instead of one waiting in the key exchange."""
+    import uuid
+    import torch.multiprocessing as mp
+    from parallelparsing_amd._lib import PPG_ARG_ERROR
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/ppg_cpu_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_pairs_no_device, args=(r, 2, name, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: PPG_ARG_ERROR, 1: PPG_ARG_ERROR}

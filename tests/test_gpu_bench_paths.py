@@ -47,7 +47,7 @@ def test_bench_paired_two_ranks_same_pairs():
     one = _bench(args)
     two = _bench(args, ranks=2)
     assert one["config"]["pairs"] == two["config"]["pairs"] == 300000
-    assert two["n_gpus"] == 2 and two["config"]["pair_check"].startswith("all_to_all")
+    assert two["n_gpus"] == 2 and two["config"]["pair_check"].startswith("ppg_pairs_check: keys to pair owners")
 
 
 def test_bench_rccl_glue_world1():
@@ -81,3 +81,18 @@ def test_bench_shares_the_input_between_ranks():
     assert st["input_how"].startswith("built (shared via /dev/shm/")
     assert len(st["per_rank"]) == 2
     assert set(glob.glob("/dev/shm/ppg_bench_*")) == before
+
+
+def test_bench_world8_rehearsal():
+    """configs[3]'s world size on the one-GPU box: `bench.py --gpus 8` starts
+    eight ranks (all on cuda:0, gloo + the library's host transport for the count gather) and runs
+    the whole N = 8 path -- ppg_partition's ranges, the per-rank auto split, gather_pairs, the count
+    gather, max-over-ranks timing -- to the single-rank record count (the bench asserts it)."""
+    one = _bench(SMALL + ["--repeats", "16"])
+    eight = _bench(SMALL + ["--repeats", "16", "--gpus", "8"], timeout=420)
+    assert eight["n_gpus"] == 8 and eight["scaling"] == "strong"
+    assert eight["config"]["workload"].startswith("configs[3]")
+    assert eight["config"]["records"] == one["config"]["records"]
+    assert eight["communicator"]["world_size"] == 8
+    assert "ppg_shard_gather_counts" in eight["communicator"]["count_gather"]
+    assert len(eight["setup_s"]["per_rank"]) == 8

@@ -70,8 +70,7 @@ def test_configs4_full_size_pair_on_one_gpu(device):
     tfs = [TiledFile(2_621_440, reps, 50_000, seed=m - 1, mate=m, threads=16) for m in (1, 2)]
     assert all(tf.file_len > 24e9 for tf in tfs)
     dev = torch.device("cuda", device.device)
-    counts = []
-    keys = []
+    shards, comps = [], []
     for tf in tfs:
         lo, hi = int(tf.p_input[0]) - 1, int(tf.p_input[-1])   # file bytes [Input_0 - 1, Input_n - 1]
         comp = torch.empty(hi - lo + 256, dtype=torch.uint8, device=dev)
@@ -88,10 +87,14 @@ def test_configs4_full_size_pair_on_one_gpu(device):
         assert (r["status"] == 0).all()
         assert (r["produced"] == np.diff(tf.p_output)).all()
         assert sh.total_records == tf.expected_records()
-        k, _ = paired.dedup(paired.shard_keys(sh))
-        keys.append(k.clone())
-        counts.append(sh.total_records)
-        del sh, comp
-        torch.cuda.empty_cache()
-    npairs = paired.check_pairs(keys[0], keys[1])
-    assert npairs == 2_621_440 * reps
+        shards.append(sh)
+        comps.append(comp)
+    # the pair check in the library (ppg_pairs_check: keys of every batch, Q1 duplicates dropped)
+    res = paired.Pairs().check(shards[0], shards[1])
+    assert res["pairs"] == 2_621_440 * reps and res["mismatches"] == 0, res
+    assert res["records"] == (2_621_440 * reps,) * 2
+    assert [sh.total_records - d for sh, d in zip(shards, res["duplicates"])] == [2_621_440 * reps] * 2
+    # the same pairing restated with torch on the keys (test-side reference)
+    k = [paired.shard_keys(sh) for sh in shards]
+    k = [x[x != paired.DUP] for x in k]
+    assert torch.equal(k[0], k[1]) and bool((k[0] >= 0).all())

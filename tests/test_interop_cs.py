@@ -63,10 +63,25 @@ def test_batch_struct_layout_matches_header():
     assert [norm(f) for f in c_fields] == [norm(f) for f in cs_fields]
 
 
+def test_pair_result_layout_matches_header():
+    """ppg_pair_result's fields in order, arrays as C# fixed buffers of the same length."""
+    h = _read("include", "ppgpu.h")
+    body = h[h.index("typedef struct {", h.index("paired reads")):h.index("} ppg_pair_result;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    c_fields = re.findall(r"int64_t (\w+)(?:\[(\d)\])?;", body)
+    cs = _read("interop", "PpGpu.cs")
+    sb = cs[cs.index("struct PpgPairResult"):]
+    sb = sb[:sb.index("}")]
+    cs_fields = re.findall(r"public (?:fixed )?long (\w+)(?:\[(\d)\])?;", sb)
+    norm = lambda x: x.replace("_", "").lower()   # noqa: E731
+    assert [(norm(a), b) for a, b in c_fields] == [(norm(a), b) for a, b in cs_fields]
+    assert len(c_fields) == 6
+
+
 # ---- type-level check: include/ppgpu.h parameter / return types -> allowed C# types ----
 _SCALAR = {"int": "int", "int32_t": "int", "int64_t": "long", "uint32_t": "uint", "float": "float",
            "double": "double"}
-_OPAQUE = {"ppg_ctx", "ppg_index", "ppg_shard", "ppg_cursor", "ppg_comm"}
+_OPAQUE = {"ppg_ctx", "ppg_index", "ppg_shard", "ppg_cursor", "ppg_comm", "ppg_pairs"}
 
 
 def _c_params():
@@ -114,6 +129,8 @@ def _allowed(ctype, ret=False):
         return {"nint"} if ret else {"string"}
     if stars == 1 and base == "ppg_batch":
         return {"out PpgBatch", "PpgBatch*"}
+    if stars == 1 and base == "ppg_pair_result":
+        return {"out PpgPairResult", "PpgPairResult*"}
     if stars == 1 and base == "void":
         return {"nint"} if ret else {"void*", "nint", "byte*"}
     if stars == 1 and base == "uint8_t":

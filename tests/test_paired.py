@@ -1,8 +1,11 @@
-"""Paired-end record-aligned pair chunks.  CPU: the distributed pair check over
-gloo (world 2); GPU: pairing two synthetic mate files against their generated text."""
+"""Paired-end record-aligned pair chunks through the C ABI's pair check
+(ppg_pairs_*, csrc/ppg_pairs.hip): two synthetic mate files against their generated text, on one
+rank and on 2 / 3 ranks of the one GPU over the library's host transport (the key exchange's
+collective is covered on the CPU in tests/test_dist.py)."""
 import ctypes as C
 import os
 import socket
+import uuid
 
 import numpy as np
 import pytest
@@ -20,39 +23,6 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
-
-
-def _worker(rank, world, port, case, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        n = 1000
-        keys = torch.arange(1, n + 1, dtype=torch.int64)
-        # the two files split differently over the ranks (their chunk boundaries differ)
-        c1, c2 = [0, 337, n], [0, 612, n]
-        k1 = keys[c1[rank]:c1[rank + 1]].clone()
-        k2 = keys[c2[rank]:c2[rank + 1]].clone()
-        if case == "swap" and rank == 1:
-            k2[5], k2[6] = k2[6].item(), k2[5].item()
-        if case == "short" and rank == 1:
-            k2 = k2[:-1]
-        q.put((rank, paired.distributed_pair_check(k1, k2)))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("case,expect", [("ok", (1000, 0)), ("swap", (1000, 2)), ("short", (999, 1))])
-def test_distributed_pair_check_gloo(case, expect):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
-    for p in ps:
-        p.join(60)
-    assert res[0] == res[1] == expect
 
 
 def _mate_file(mate, seed, nrec, tmp_path):
@@ -141,10 +111,13 @@ def test_record_keys_drop_q1_duplicates(tmp_path):
     _, i1, _, _ = ix.point_fields(n)
     sh = pp.Shard(ix, np.frombuffer(gz[i0 - 1:i1], np.uint8), 0, n).run()
     keys = paired.shard_keys(sh)
-    kept, _ = paired.dedup(keys)
+    kept = keys[keys != paired.DUP]
     assert sh.total_records > nrec                       # the reference's duplicates are there
     assert int((keys == paired.DUP).sum()) == sh.total_records - nrec
     assert torch.equal(kept.cpu(), torch.arange(1, nrec + 1))
+    # the library's pair check drops the same records: the file pairs with itself, nrec pairs
+    res = paired.Pairs().check(sh, sh)
+    assert res["pairs"] == nrec and res["mismatches"] == 0 and res["duplicates"] == (sh.total_records - nrec,) * 2
     # the same keys with every chunk split at its inner block start (bench --paired's auto split)
     from test_gpu_parity import dense_side_points
     bits, outs, win = dense_side_points(gz, ix)
@@ -225,3 +198,96 @@ def test_record_keys_identifier_edge_cases(chunk, device):
     assert got == exp
     assert exp.count(-1) > 100 and 123456789012345678 in exp   # Q1 (-2): test_record_keys_drop_q1_duplicates
     assert {1000 + i for i in range(0, 600, len(HEADERS))} <= set(exp)   # ordinary keys decoded
+
+
+def _text_gz(txt):
+    S = pp.synth()
+    a = np.frombuffer(txt, np.uint8)
+    gzb = np.zeros(a.size, np.uint8)
+    L = S.ppg_synth_gzip(C.c_void_p(a.ctypes.data), a.size, 6, 1 << 20, 8, C.c_void_p(gzb.ctypes.data), gzb.size)
+    return gzb[:L].tobytes()
+
+
+def _pair_files(tmp_path, nrec, case):
+    """R1 / R2 mate files; case 'swap' exchanges R2's records 5000 and 5001, 'short' drops R2's last."""
+    p1, _ = _mate_file(1, 0, nrec, tmp_path)
+    _, t2 = _mate_file(2, 1, nrec, tmp_path)
+    lines = t2.split(b"\n")[:-1]
+    recs = [b"\n".join(lines[4 * i:4 * i + 4]) + b"\n" for i in range(nrec)]
+    if case == "swap":
+        recs[5000], recs[5001] = recs[5001], recs[5000]
+    if case == "short":
+        recs = recs[:-1]
+    p2 = tmp_path / f"r2_{case}.fastq.gz"
+    p2.write_bytes(_text_gz(b"".join(recs)))
+    return p1, str(p2)
+
+
+EXPECT = {"ok": (30_000, 0, -1), "swap": (30_000, 2, 5000), "short": (29_999, 1, 29_999)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["ok", "swap", "short"])
+def test_pairs_check_one_rank(case, tmp_path, device):
+    p1, p2 = _pair_files(tmp_path, 30_000, case)
+    shards = []
+    for p, chunk in ((p1, 700), (p2, 1100)):
+        ix = pp.Core.BuildDeflateIndex(p, chunk)
+        n = ix.Count - 1
+        shards.append(pp.Shard(ix, paired._read_range(p, ix), 0, n, device=device).run())
+    pr = paired.Pairs()
+    res = pr.check(shards[0], shards[1])
+    assert (res["pairs"], res["mismatches"], res["first_bad"]) == EXPECT[case], res
+    if case == "swap":
+        assert res["first_keys"] == (5001, 5002)
+    if case == "ok":
+        assert (pr.records(0, 0, 30_000) == np.arange(30_000)).all()   # no Q1 duplicates in these files
+
+
+def _pair_rank(rank, world, name, p1, p2, q):
+    try:
+        import parallelparsing_amd as pp2
+        from parallelparsing_amd import paired as P
+        dev = pp2.Device(0)
+        comm = pp2.Comm.host(world, rank, name)
+        shards = []
+        for p, chunk in ((p1, 700), (p2, 1100)):   # the files' rank ranges never line up
+            ix = pp2.Core.BuildDeflateIndex(p, chunk)
+            b = pp2.partition(ix, world)
+            a, e = int(b[rank]), int(b[rank + 1])
+            _, i0, _, _ = ix.point_fields(a)
+            _, i1, _, _ = ix.point_fields(e)
+            with open(p, "rb") as f:
+                f.seek(i0 - 1)
+                comp = np.frombuffer(f.read(i1 - i0 + 1), np.uint8)
+            shards.append(pp2.Shard(ix, comp, a, e - a, device=dev).run())
+        pr = P.Pairs()
+        res = pr.check(shards[0], shards[1], comm)
+        res2 = pr.check(shards[0], shards[1], comm)      # reused scratch, same answer
+        comm.close()
+        q.put((rank, res, res2 == res))
+    except Exception as e:   # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e), False))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,case", [(2, "ok"), (2, "swap"), (3, "short"), (3, "ok")])
+def test_pairs_check_multi_rank_on_one_gpu(world, case, tmp_path, device):
+    """ppg_pairs_check on `world` processes of the box's one GPU over the host transport: each rank
+    decodes its own chunk ranges of R1 and R2, every key moves to its pair's owner
+    (ppg_comm_alltoallv), and every rank gets the single-rank result."""
+    import torch.multiprocessing as mp
+    p1, p2 = _pair_files(tmp_path, 30_000, case)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/ppg_test_{uuid.uuid4().hex[:12]}"
+    procs = [ctx.Process(target=_pair_rank, args=(r, world, name, p1, p2, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for pr in procs:
+        pr.join(60)
+    for r in res:
+        assert isinstance(r[1], dict), r
+        assert (r[1]["pairs"], r[1]["mismatches"], r[1]["first_bad"]) == EXPECT[case], r
+        assert r[2]

@@ -8,7 +8,7 @@
 # Outputs gpurun_out/r04_<tag>.json (+ .log).  Stops at the first failing run.
 set -o pipefail
 mkdir -p gpurun_out
-summ() { python3 -c "import json; d=json.load(open('gpurun_out/r04_$1.json')); print('$1', d['n_gpus'], round(d['value']/1e6,1), 'Mrec/s', round(d['ms_per_step'],2), 'ms', {k: round(v,2) for k,v in d['kernel_ms_per_step'].items()}, d['config'].get('waves_per_chunk'))"; }
+summ() { python3 -c "import json; d=json.loads([l for l in open('gpurun_out/r04_$1.json') if l.startswith('{')][-1]); print('$1', d['n_gpus'], round(d['value']/1e6,1), 'Mrec/s', round(d['ms_per_step'],2), 'ms', {k: round(v,2) for k,v in d['kernel_ms_per_step'].items()}, d['config'].get('waves_per_chunk'))"; }
 if [ -z "$SKIP_W8" ]; then
   PPG_BENCH_ONE_DEVICE=1 PPG_DIST_BACKEND=gloo timeout -k 10 400 python3 -u bench.py --gpus 8 --seg-records 40000 \
     --repeats 16 --steps 2 --warmup 1 --no-cpu-baseline --no-ingest > gpurun_out/r04_w8.json 2> gpurun_out/r04_w8.log || exit $?
@@ -21,9 +21,14 @@ run() {
   summ $tag
 }
 [ -z "$SKIP_N1" ] && run n1
-for n in ${SHARES:-2 4 8}; do run share$n --share $n; done
+for n in ${SHARES-2 4 8}; do run share$n --share $n; done
 for spec in ${SHARE8_VARIANTS}; do
   a=${spec#*:}
   run "s8_${spec%%:*}" --share 8 ${a//_/ }
+done
+# VARIANTS: tag:args items for any share ('_' stands for a space inside args)
+for spec in ${VARIANTS}; do
+  a=${spec#*:}
+  run "v_${spec%%:*}" ${a//_/ }
 done
 exit 0
