@@ -566,8 +566,9 @@ def auto_split(args, slots, chunks):
 
 def tail2_split(args, slots, ksplit):
     """(S2, K2): of the K split chunks, the last K2 into up to S2 waves each (--tail2 S2:G2, default
-    16 for the last quarter generation: the launch drains on pieces of ~1/16 chunk; "off" = none).
-    Measured: the N = 8 share 111.4 -> 108.5 ms, N = 2 / 4 0.5 - 0.8% faster."""
+    64 for the last quarter generation: the launch drains on pieces of single deflate blocks; "off"
+    = none).  Measured (DESIGN.md §5, r04 on the r03 v5 kernel): the N = 8 share 91.3 (16) / 88.5
+    (32) -> 86.9 ms (64), N = 1 688.8 -> 684.9, N = 2 / 4 346.3 / 188.9 -> 341.2 / 171.3 ms."""
     if not args.tail2 or args.tail2 == "off":
         return args.split, 0
     s2, g2 = args.tail2.split(":")
@@ -695,9 +696,9 @@ def main():
     ap.add_argument("--paired-out-gib", type=float, default=56.0,
                     help="--paired: output buffer per file in GiB (a rank's range decodes in batches of this; the "
                          "spot keys are extracted per batch)")
-    ap.add_argument("--tail2", default="16:0.25",
+    ap.add_argument("--tail2", default="64:0.25",
                     help="S2:G2 -- of the split chunks, the last G2 generations into up to S2 waves each "
-                         "(default 16:0.25; off = none)")
+                         "(default 64:0.25, in practice every inner block start; off = none)")
     ap.add_argument("--split-gens", type=float, default=1,
                     help="--split 0: a rank with fewer chunks than this many generations of wave slots splits every "
                          "chunk; a larger one splits its last --tail-gens generations into --tail-split waves")

@@ -41,10 +41,10 @@ def test_tail_knobs():
 
 def test_tail2_split():
     a = args()
-    a.tail2 = "16:0.25"
+    a.tail2 = "64:0.25"                                         # the default since r04 (16 before)
     a.split = 8
-    assert bench.tail2_split(a, SLOTS, 4096) == (16, 2048)     # N = 1: the last quarter generation into 16
-    assert bench.tail2_split(a, SLOTS, 1000) == (16, 1000)     # fewer split chunks than that: all of them
+    assert bench.tail2_split(a, SLOTS, 4096) == (64, 2048)     # N = 1: the last quarter generation into 64
+    assert bench.tail2_split(a, SLOTS, 1000) == (64, 1000)     # fewer split chunks than that: all of them
     a.tail2 = "off"
     assert bench.tail2_split(a, SLOTS, 4096) == (8, 0)
     a.tail2, a.split = "4:0.25", 8                              # not finer than the split: no second stage
