@@ -39,52 +39,21 @@
 // before r03; ppg_resolve_kernel turns the tails into exact histories.
 #define IX_RING_BYTES 65536u
 #define IX_RING_MASK (IX_RING_BYTES - 1u)
-#define PPG_STR2(x) #x
-#define PPG_STR(x) PPG_STR2(x)
-// Wave priority (s_setprio) by phase of the token round: the decode (PPG_DEC_PRIO, default none =
-// 0), the serial walk (PPG_WALK_PRIO) and after it until the round's bytes are written
-// (PPG_EMIT_PRIO), held through the round's tail (PPG_TAIL_PRIO: pos/carry/flush) and dropped to 0
-// before the next round's decode.  A wave that has walked its round finishes it ahead of waves
-// still decoding theirs: the walk and the emit are one serial chain of dependent LDS / lane /
-// far-load latencies, the decode is VALU-dense and latency-tolerant.  Measured on the 50 GB step
-// (tools/ab_bench.sh, r02): none 840.4 ms; walk 2: 815-818; walk 2 + emit 1: 794.7; + tail: 793.3;
-// walk 1 + emit 1: 795.2; decode 1 as well: 846.4 (priority on the decode costs what it gains).
-// PPG_NO_PRIO builds the kernel without any of it.
-#ifndef PPG_NO_PRIO
-#ifndef PPG_WALK_PRIO
-#define PPG_WALK_PRIO 2
-#endif
-#ifndef PPG_EMIT_PRIO
-#define PPG_EMIT_PRIO 1
-#endif
-#ifndef PPG_TAIL_PRIO
-#define PPG_TAIL_PRIO 1
-#endif
-// the other serial stretches of the decoder: a bit-serial token (long code, end-of-block) and a
-// dynamic block header (code lengths, tables): 810.1 -> 805.9 ms with both at 2 (r02, near noise)
-#ifndef PPG_SPEC_PRIO
-#define PPG_SPEC_PRIO 2
-#endif
-#ifndef PPG_HDR_PRIO
-#define PPG_HDR_PRIO 2
-#endif
-#endif
-#ifndef PPG_POST_WALK_PRIO
-#ifdef PPG_EMIT_PRIO
-#define PPG_POST_WALK_PRIO PPG_EMIT_PRIO
-#else
-#define PPG_POST_WALK_PRIO 0
-#endif
-#endif
+// Wave priority (s_setprio) by phase of the token round: 2 for the serial walk, 1 after it until
+// the round's bytes are written and through the round's tail (pos/carry/flush), 0 again before the
+// next round's decode.  A wave that has walked its round finishes it ahead of waves still decoding
+// theirs: the walk and the emit are one serial chain of dependent LDS / lane / far-load latencies,
+// the decode is VALU-dense and latency-tolerant.  Measured on the 50 GB step (tools/ab_bench.sh,
+// r02): none 840.4 ms; walk 2: 815-818; walk 2 + emit 1: 794.7; + tail: 793.3; walk 1 + emit 1:
+// 795.2; decode 1 as well: 846.4 (priority on the decode costs what it gains).  The other serial
+// stretches -- a bit-serial token (long code, end-of-block) and a dynamic block header -- run at 2:
+// 810.1 -> 805.9 ms (r02, near noise).  (r03 re-tried emit 2 / walk 3: no gain,
+// profiles/r03_ab_walk_prio_variants.txt.)
 
 template <int RB, int LBT, typename RingT = uint8_t>
 struct __attribute__((aligned(16))) InflateLds {
     // first: the decode's five-word reads address it with ds_read2 offsets (8-bit dword fields)
-#ifdef PPG_WORDS6
-    uint32_t stream[136];          // compressed words: segment g (32 words) at slot g & 3; [128,134) mirror [0,6)
-#else
     uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
-#endif
     RingT ring[1u << RB];          // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1)
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LBT];
@@ -118,15 +87,6 @@ __device__ unsigned long long ppg_stamp_acc[8];
 #define PPG_STAMP(t)
 #endif
 
-// branch-layout hints for the token round (PPG_LIKELY builds): the hot path as fall-through code
-#ifdef PPG_LIKELY
-#define PPG_HOT(c) __builtin_expect(!!(c), 1)
-#define PPG_COLD(c) __builtin_expect(!!(c), 0)
-#else
-#define PPG_HOT(c) (c)
-#define PPG_COLD(c) (c)
-#endif
-
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
@@ -158,11 +118,7 @@ struct Reader {
 // only by st_enter's explicit s_waitcnt; an untracked VMEM op can only make the compiler's own
 // vmcnt waits stricter, never looser.  (s_nop: SALU write of M0 -> LDS DMA needs one wait state.)
 __device__ __forceinline__ void lds_dma_dword(const uint32_t *src, const uint32_t *lds_base) {
-#ifdef PPG_STREAM_NT
-    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off nt" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)lds_base)
-#else
     asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "{m0}"((uint32_t)(uintptr_t)lds_base)
-#endif
                  : "memory");
 }
 
@@ -170,17 +126,13 @@ __device__ __forceinline__ void st_issue(const Reader &r, uint32_t *stream, uint
     const uint32_t i = min(g * 32 + (uint32_t)lane, r.nw - 1);   // past the end: any valid word
     if (lane < 32) lds_dma_dword(r.base + i, stream + (g & 3) * 32);
     // slot 0's first words again after slot 3, so a lane's consecutive words never wrap
-#ifdef PPG_WORDS6
-    if ((g & 3) == 0 && lane < 6) lds_dma_dword(r.base + i, stream + 128);
-#else
     if ((g & 3) == 0 && lane < 4) lds_dma_dword(r.base + i, stream + 128);
-#endif
 }
 
 // make segments g and g+1 resident (g+2 loading).  g == sg - 1 is resident too (the bit reader
 // runs up to two words ahead of the decode position and may have entered sg already).
 __device__ __forceinline__ void st_enter(Reader &r, uint32_t *stream, uint32_t g, int lane) {
-    if (PPG_HOT(g == r.sg || g + 1 == r.sg)) return;
+    if (g == r.sg || g + 1 == r.sg) return;
     if (g != r.sg + 1) {
         st_issue(r, stream, g, lane);
         st_issue(r, stream, g + 1, lane);
@@ -330,11 +282,7 @@ __device__ __forceinline__ void census_step(uint32_t *cen, const CensusOut &co, 
             if (mm) {
                 const uint32_t b = (uint32_t)__builtin_ctz(mm);
                 mm &= mm - 1u;
-#ifdef PPG_CENSUS_NT
-                if (idx < co.cap) __builtin_nontemporal_store(co.shift + p_lane + b, co.dst + idx);
-#else
                 if (idx < co.cap) ((__attribute__((address_space(1))) uint32_t *)co.dst)[idx] = co.shift + p_lane + b;
-#endif
                 idx++;
             }
         }
@@ -374,9 +322,7 @@ __device__ __forceinline__ void flush_census(const uint8_t *ring, uint8_t *out, 
             nact = min(left / 16, 64u);
             if ((uint32_t)lane < nact) {
                 const uint4 v = *(const uint4 *)(ring + ((uint32_t)(g + 16 * lane) & RM));
-#ifndef PPG_PROBE_NO_STORE   // timing probe only (A/B): no output stores, far bytes read garbage
                 *(uint4 *)(out + g + 16 * lane) = v;
-#endif
                 w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
             }
             lastbit = 15;
@@ -424,34 +370,16 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, con
 // No wait states precede the load: the base pair must not be written by a VALU (a spill restore)
 // just before it -- tools/hazard_lint.py checks the compiled kernel for that at every build (with
 // amdgpu_num_sgpr(64) the base was spilled and the load faulted; padding costs 0.6%).
-// PPG_FAR_NOP pads the load with the 5 wait states (builds whose SGPR pressure spills the base).
-#ifdef PPG_FAR_NOP
-#define PPG_FAR_PAD "s_nop 4\n\t"
-#else
-#define PPG_FAR_PAD ""
-#endif
 __device__ __forceinline__ uint32_t far_load(const uint8_t *base, uint32_t off) {
     uint32_t v;
-    asm volatile(PPG_FAR_PAD "global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+    asm volatile("global_load_dword %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
     return v;
 }
 // the byte itself (DecompressAll's emit): no alignment mask, no bit-field extract (r03 v4:
 // 707 -> 698.5 ms per 50 GB step, same-box A/B)
 __device__ __forceinline__ uint32_t far_load_u8(const uint8_t *base, uint32_t off) {
     uint32_t v;
-    asm volatile(PPG_FAR_PAD "global_load_ubyte %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
-    return v;
-}
-
-// far_load in two halves (PPG_FAR_SPLIT): the load, and the wait that hands its result over.  The
-// value is an in/out operand of the wait, so nothing reads it before the load has landed.
-__device__ __forceinline__ uint32_t far_issue(const uint8_t *base, uint32_t off) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, %2" : "=&v"(v) : "v"(off), "s"(base) : "memory");
-    return v;
-}
-__device__ __forceinline__ uint32_t far_wait(uint32_t v) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : : "memory");
+    asm volatile("global_load_ubyte %0, %1, %2\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(off), "s"(base) : "memory");
     return v;
 }
 
@@ -532,28 +460,6 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 template <uint32_t STOPMASK = 0x1C0C0u>
 __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
     uint32_t t, tmp;
-#ifdef PPG_WALK_UNROLL
-    // two tokens per loop trip: the first token's stop test leaves by a not-taken-usually branch,
-    // so a walk of n tokens takes ~n/2 taken branches instead of n
-    asm volatile(
-        "1:\n\t"
-        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], %[M]\n\t"
-        "v_writelane_b32 %[vtin], %[t], m0\n\t"
-        "s_cbranch_scc1 2f\n\t"
-        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], %[M]\n\t"
-        "v_writelane_b32 %[vtin], %[t], m0\n\t"
-        "s_cbranch_scc0 1b\n"
-        "2:"
-        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
-        : [vt] "v"(vt), [M] "i"(STOPMASK)
-        : "m0", "scc");
-#else
     asm volatile(
         "1:\n\t"
         "v_readlane_b32 %[t], %[vt], %[X]\n\t"
@@ -565,38 +471,11 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
         : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
         : [vt] "v"(vt), [M] "i"(STOPMASK)
         : "m0", "scc");
-#endif
 }
 
-// The walk two tokens per step (PPG_WALK_PAIR): vt2[c] is the token word of the candidate right
-// after c's token (c + bits(c)), gathered once per span by one ds_bpermute, so a step reads both
-// tokens at once and the walk's serial chain -- v_readlane -> s_add -> v_readlane, ~75 cycles per
-// token on gfx950 even for a wave alone on its SIMD (tools/walk_lat.hip) -- is paid once per two
-// tokens.  The first token is placed and tested as before; a step whose first token already ends
-// the walk leaves without placing the second (its lane select would wrap), so X, the placed tokens
-// and the stop are exactly walk_asm's.
-template <uint32_t STOPMASK = 0x1C0C0u>
-__device__ __forceinline__ void walk_asm_pair(uint32_t vt, uint32_t vt2, uint32_t &vtin, uint32_t &X) {
-    uint32_t t, u, tmp;
-    asm volatile(
-        "1:\n\t"
-        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
-        "v_readlane_b32 %[u], %[vt2], %[X]\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], %[M]\n\t"
-        "v_writelane_b32 %[vtin], %[t], m0\n\t"
-        "s_cbranch_scc1 2f\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[u], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], %[M]\n\t"
-        "v_writelane_b32 %[vtin], %[u], m0\n\t"
-        "s_cbranch_scc0 1b\n"
-        "2:"
-        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [u] "=&s"(u), [tmp] "=&s"(tmp)
-        : [vt] "v"(vt), [vt2] "v"(vt2), [M] "i"(STOPMASK)
-        : "m0", "scc");
-}
+// (r03 tried a walk taking two tokens per step -- each candidate's following token gathered by one
+// ds_bpermute per span, the v_readlane -> s_add -> v_readlane chain paid once per two tokens:
+// 829.1 vs 802.0 ms; an unrolled two-token loop: 799.4 vs 802.4.  DESIGN.md §4.)
 
 // IX = false: Core.ExtractDeflateIndex of checkpoint chunks (out_len bytes each).
 // IX = true:  CreateIndex pass 1 (ppg_index_gpu.cpp): decode whole blocks from a candidate block
@@ -605,23 +484,9 @@ __device__ __forceinline__ void walk_asm_pair(uint32_t vt, uint32_t vt2, uint32_
 // needed for 8 waves per SIMD (97 gives 6; MI355X_MICROARCH.md, occupancy formula)
 // r03 v4: the token rounds as an inner loop with one latch, and the emit's token-start address as
 // one v_mad_i32_i24 -- together 694.5 -> 682.2 ms per 50 GB step (each alone: 695.1 / 701.0;
-// profiles/r03_ab_latch_sj.txt).  PPG_TWO_EXITS / PPG_SJ_SHIFT build the previous forms.
-#if !defined(PPG_TWO_EXITS) && !defined(PPG_ONE_LATCH)
-#define PPG_ONE_LATCH
-#endif
-#if !defined(PPG_SJ_SHIFT) && !defined(PPG_SJ_MAD)
-#define PPG_SJ_MAD
-#endif
-#ifndef PPG_NUM_SGPR
-#define PPG_NUM_SGPR 80
-#endif
+// profiles/r03_ab_latch_sj.txt).
 template <int RB, int LBT, bool IX, bool CEN>
-#ifdef PPG_NUM_VGPR
-#define PPG_VGPR_ATTR __attribute__((amdgpu_num_vgpr(PPG_NUM_VGPR), amdgpu_waves_per_eu(8, 8)))
-#else
-#define PPG_VGPR_ATTR
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) PPG_VGPR_ATTR void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
@@ -798,9 +663,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             build_table<DB>(S.lens + 288, 32, S.dst, &cdst, S.dst_sorted, TAB_DST, lane);
         } else {
             // ---- dynamic Huffman codes (RFC 1951 3.2.7) ----
-#ifdef PPG_HDR_PRIO
-            asm volatile("s_setprio " PPG_STR(PPG_HDR_PRIO));
-#endif
+            asm volatile("s_setprio 2");
             rd_refill(r, S.stream, lane);
             const uint32_t hlit = br_take(r, 5) + 257, hdist = br_take(r, 5) + 1, hclen = br_take(r, 4) + 4;
             if (hlit > 286 || hdist > 30) { status = ST_DATA_ERROR; break; }
@@ -843,9 +706,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, &cdst, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
         }
         in_block = 1;
-#ifdef PPG_HDR_PRIO
         asm volatile("s_setprio 0");
-#endif
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
         // through the outer loop), so the token rounds keep it in SGPRs with scalar branches
         r.sg = uni(r.sg);
@@ -875,37 +736,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
         struct Words { uint32_t x0, x1, x2, x3, x4; };
         auto words = [&](uint32_t bp) -> Words {
             const uint32_t o = (bp & 31) + (uint32_t)lane;                      // 0..94
-#ifdef PPG_WORDS6
-            // the wrap applied to the uniform part only: a lane's words end at most at 127 + 2 + 4
-            const uint32_t *sw = S.stream + (((bp >> 5) & 127) + (o >> 5));
-#else
             const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
-#endif
             return Words{sw[0], sw[1], sw[2], sw[3], sw[4]};
         };
-#ifdef PPG_NO_WORD_PREFETCH
-        auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos) -> Round {
-#else
         auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos, const Words &W) -> Round {
-#endif
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t vtin = 0;
-#ifdef PPG_CARRY_ALWAYS
-            vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);   // cw = 0 without a carry
-#else
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
-#endif
             bool spec = false;
             if (off < min(64u, len - pos)) {
-#ifdef PPG_DEC_PRIO
-                asm volatile("s_setprio " PPG_STR(PPG_DEC_PRIO));
-#endif
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring, read during the previous round's emit)
                 const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
-#ifdef PPG_NO_WORD_PREFETCH
-                const Words W = words(bp);
-#endif
                 const uint32_t x0 = W.x0, x1 = W.x1, x2 = W.x2, x3 = W.x3, x4 = W.x4;
                 // speculative tokens at every bit offset of the 128-bit span (two per lane)
                 const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
@@ -928,64 +770,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
 #ifdef PPG_STAMPS
                 st_w0 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(vta ^ vtb);
 #endif
-                if (PPG_HOT(len - pos >= 64)) {
+                if (len - pos >= 64) {
                     X = off << 8;
-#ifdef PPG_WALK_PRIO
-                    asm volatile("s_setprio " PPG_STR(PPG_WALK_PRIO));
-#endif
-#if defined(PPG_WALK_C)
-                    do {
-                        t = rdlane(vta, X);
-                        vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
-                        X += t;
-                    } while ((X & STOP) == 0u);
-                    if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
-                        X -= 64;
-                        half = 64;
-                        do {
-                            t = rdlane(vtb, X);
-                            vtin = (uint32_t)llvm_writelane((int)t, (int)(X >> 8), (int)vtin);
-                            X += t;
-                        } while ((X & STOP) == 0u);
-                    }
-#elif defined(PPG_WALK_CONT)
-                    // s runs on through the second span (v_readlane uses s[5:0] = s - 64 there):
-                    // that walk stops at s >= 128 (bit 7) or off >= 64; a special token in it
-                    // leaves s >= 192, one in the first span s in [128, 192) -- no rebasing
-                    walk_asm(vta, vtin, X);
-                    if ((X & (STOP & ~0x40u)) == 0u) {
-                        walk_asm<0x1C080u>(vtb, vtin, X);
-                        const bool sp2 = (X & 0xC0u) == 0xC0u;
-                        off = (X >> 8) & 511u;
-#ifdef PPG_WALK_PRIO
-                        asm volatile("s_setprio " PPG_STR(PPG_POST_WALK_PRIO));
-#endif
-                        return Round{vtin, off, (X & 255u) - (sp2 ? 128u : 0u), sp2};
-                    }
-#elif defined(PPG_WALK_PAIR)
-                    {
-                        // each candidate's following token (wraps past lane 63: such a first token
-                        // ends the span, so the second is never used)
-                        const uint32_t vta2 = bperm(((uint32_t)lane + (vta & 255u)) << 2, vta);
-                        const uint32_t vtb2 = bperm(((uint32_t)lane + (vtb & 255u)) << 2, vtb);
-                        walk_asm_pair(vta, vta2, vtin, X);
-                        if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
-                            X -= 64;
-                            half = 64;
-                            walk_asm_pair(vtb, vtb2, vtin, X);
-                        }
-                    }
-#else
+                    asm volatile("s_setprio 2");
                     walk_asm(vta, vtin, X);
                     if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
                         X -= 64;
                         half = 64;
                         walk_asm(vtb, vtin, X);
                     }
-#endif
-#ifdef PPG_WALK_PRIO
-                    asm volatile("s_setprio " PPG_STR(PPG_POST_WALK_PRIO));
-#endif
+                    asm volatile("s_setprio 1");
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -1012,29 +806,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             return Round{vtin, off, s, spec};
         };
 
-#ifndef PPG_NO_WORD_PREFETCH
         st_enter(r, S.stream, bp >> 10, lane);
         Words W = words(bp);
-#endif
         for (;;) {
-#ifdef PPG_ONE_LATCH
           // the token rounds as an inner loop with ONE latch (not special, output left): the two
           // exits of the plain form made the compiler merge them through an exit-selector register
           bool spec_ = false;
           do {
-#endif
             // ---- one round: decode + walk, then one output byte per lane ----
             PPG_STAMP(t0);
-#ifdef PPG_NO_WORD_PREFETCH
-            st_enter(r, S.stream, bp >> 10, lane);
-            const Round R = decode(bp, cn, cw, pos);
-#else
             const Round R = decode(bp, cn, cw, pos, W);
             // the next round's stream words, read now: their LDS latency overlaps this round's
             // emit instead of opening the next round's chain of dependent LDS reads (r03)
             st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
             W = words(bp + R.adv);
-#endif
 #ifdef PPG_STAMPS
             const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
             if (st_w0 < t0) st_w0 = t1;   // no walk this round
@@ -1056,30 +841,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
             // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
             {
-#ifdef PPG_SJ_MAD
                 // 4 * (63 - clz) in one v_mad_i32_i24 (the compiler's form: shift + xor)
                 uint32_t sj4;
                 asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
                 const uint32_t inf = bperm(sj4, R.vtin);
-#else
-                const uint32_t sj = 63u - (uint32_t)__builtin_clzll(mo & lanes_le);   // start of this byte's token
-                const uint32_t inf = bperm(sj << 2, R.vtin);
-#endif
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
-#ifdef PPG_FAR_SPLIT
-                // the far load goes out before the ring read, so the two latencies overlap
-                const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
-                const uint64_t fm = __ballot(far);
-                const int32_t fp = (int32_t)pos + jj;
-                const uint32_t fq = IX ? 2u * ((uint32_t)fp & IX_RING_MASK) : oa + (uint32_t)fp;   // byte offset
-                uint32_t fw = 0;
-                if (fm) fw = far_issue(ob, far && fp >= 0 ? (fq & ~3u) : 0u);
-                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val;   // (IX: a literal is the symbol 0x8000 | byte; written apart, the DecompressAll
-                                // instance's code is unchanged -- the folded "| 0" moved its schedule)
-                if constexpr (IX) val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
-                else val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-#else
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 uint32_t val;   // (IX: a literal is the symbol 0x8000 | byte; written apart, the DecompressAll
                                 // instance's code is unchanged -- the folded "| 0" moved its schedule)
@@ -1087,7 +853,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 else val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
                 const uint64_t fm = __ballot(far);
-#endif
 #ifdef PPG_STATS
                 if (fm) st_far++;
 #endif
@@ -1095,20 +860,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 const uint64_t t2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
                 sa_rd += t2 - t1;
 #endif
-#ifdef PPG_PROBE_NO_FAR
-                if (false) {   // timing probe only: far bytes read from the ring (wrong output)
-#else
-                if (PPG_HOT(fm)) {
-#endif
+                if (fm) {
                     // older than the ring: the flushed output (this wave's own earlier stores), as
                     // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
                     // juggling); references into the Point's window (first 32 KiB only) separately
-#ifdef PPG_FAR_SPLIT
-                    const int32_t p = fp;
-                    const uint32_t q = fq;
-                    const bool fo = far && p >= 0;
-                    const uint32_t w = far_wait(fw);
-#else
                     const int32_t p = (int32_t)pos + jj;
                     const bool fo = far && p >= 0;
                     if constexpr (IX) {
@@ -1120,14 +875,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                         const uint32_t b = far_load_u8(ob, fo ? (uint32_t)jj + (pos + oa) : 0u);
                         val = fo ? b : val;
                     }
-#endif
-#ifdef PPG_FAR_SPLIT
-                    // (bit-field offset q << 3: the instruction reads its low 5 bits, 8 * (q & 3))
-                    val = fo ? __builtin_amdgcn_ubfe(w, q << 3, IX ? 16u : 8u) : val;
-#endif
                     const bool fd = far && p < 0;
                     const uint64_t dm = fm & __ballot(p < 0);   // (a ballot of fd itself went through two VALU)
-                    if (PPG_COLD(dm)) {   // rare: the chunk's first 32 KiB
+                    if (dm) {   // rare: the chunk's first 32 KiB
                         uint32_t db;
                         if constexpr (IX) db = 32768u + (uint32_t)p;          // the history symbol itself
                         else db = dict[fd ? 32768u + (uint32_t)p : 0u];       // p >= -32768
@@ -1140,7 +890,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 sa_farr += fm ? 1 : 0;
 #endif
                 const bool dep = jj >= 0;                             // produced in this round
-                if (PPG_COLD(__ballot(dep))) {
+                if (__ballot(dep)) {
                     // chains inside the round (short distances): pointer doubling to a resolved byte
                     int32_t ptr = dep ? jj : lane;
 #ifdef PPG_STATS
@@ -1156,50 +906,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                     }
                     val = bperm((uint32_t)ptr << 2, val);
                 }
-#if defined(PPG_PAD_VALU) || defined(PPG_PAD_SALU)
-                {   // issue-bound probe (A/B only): extra independent VALU or SALU per round
-                    uint32_t pv = (uint32_t)lane, ps = pos;
-#ifdef PPG_PAD_VALU
-#pragma unroll
-                    for (int q = 0; q < PPG_PAD_VALU; q++) asm volatile("v_mov_b32 %0, %0" : "+v"(pv));
-#endif
-#ifdef PPG_PAD_SALU
-#pragma unroll
-                    for (int q = 0; q < PPG_PAD_SALU; q++) asm volatile("s_mov_b32 %0, %0" : "+s"(ps));
-#endif
-                    val += (pv ^ (uint32_t)lane) + (ps ^ pos);
-                }
-#endif
                 S.ring[(rb0 + pos + lane) & RM] = (RingT)val;
 #ifdef PPG_STAMPS
                 const uint64_t t4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
                 sa_dep += t4 - t3;
                 st_w0 = t4;   // reused below: start of the round's tail
 #endif
-#if (defined(PPG_DEC_PRIO) || defined(PPG_EMIT_PRIO)) && !defined(PPG_TAIL_PRIO)
-                asm volatile("s_setprio 0");
-#endif
             }
             cn = tot - rout;
             if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
                 cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
             }
-#ifdef PPG_CARRY_ALWAYS
-            else cw = 0;
-#endif
             pos += rout;
-            if (PPG_COLD(pos >= fl_next)) {
-#ifdef PPG_FLUSH_PRIO
-                asm volatile("s_setprio " PPG_STR(PPG_FLUSH_PRIO));
-#endif
+            if (pos >= fl_next) {
                 flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
             bp += R.adv;
-#ifdef PPG_TAIL_PRIO
             asm volatile("s_setprio 0");
-#endif
             if constexpr (IX) {   // past the member, or runaway output (a false start)
                 if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
             }
@@ -1207,21 +932,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
             sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
             st_w0 = 0;
 #endif
-#ifdef PPG_ONE_LATCH
             spec_ = R.spec;
-          } while (PPG_HOT(!spec_ && pos < len));
+          } while (!spec_ && pos < len);
             if (!spec_) break;
-#else
-            if (PPG_HOT(!R.spec)) {
-                if (PPG_HOT(pos < len)) continue;
-                break;
-            }
-#endif
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
-#ifdef PPG_SPEC_PRIO
-            asm volatile("s_setprio " PPG_STR(PPG_SPEC_PRIO));
-#endif
+            asm volatile("s_setprio 2");
             rd_seek(r, S.stream, bp, lane);
             rd_refill(r, S.stream, lane);
             const int sym = canon_decode(r, clit, S.lit_sorted, lane);
@@ -1252,13 +968,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(PPG_NUM_SGPR))) 
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
-#ifndef PPG_NO_WORD_PREFETCH
             st_enter(r, S.stream, bp >> 10, lane);
             W = words(bp);
-#endif
-#ifdef PPG_SPEC_PRIO
             asm volatile("s_setprio 0");
-#endif
             if (pos >= len) break;
         }
         if (status != ST_OK) break;
