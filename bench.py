@@ -51,9 +51,14 @@ def shared_tiled(args, key, build):
     t = time.time()
     if args.world == 1:
         return build(), time.time() - t, "built"
-    job = os.environ.get("TORCHELASTIC_RUN_ID", "") + "_" + os.environ.get("MASTER_PORT", "")
-    import hashlib   # (str hashes are salted per process: every rank must derive the same name)
-    d = os.path.join(args.shm_dir, "ppg_bench_" + hashlib.sha1(repr((job, key)).encode()).hexdigest()[:12])
+    # a name no earlier (crashed) run can have left behind: a nonce from rank 0, broadcast (ADVICE
+    # r03: a stale 'ready' of a deterministic name let ranks map files being rewritten)
+    import hashlib
+    import uuid
+    import torch.distributed as dist
+    nonce = [uuid.uuid4().hex if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(nonce, 0)
+    d = os.path.join(args.shm_dir, "ppg_bench_" + hashlib.sha1(repr((nonce[0], key)).encode()).hexdigest()[:12])
     args.shm_paths.append(d)
     if args.local_rank == 0:
         tf = build()

@@ -245,7 +245,11 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
  * Decompressor/BatchedFASTQ.cs:29-101 (IEnumerable<FastqRecord> over a bounded record cache fed by
  * LazyFileReader's partition queue, LazyFileReader.cs:41-97) over the GPU path, in bounded memory:
  * chunks [first, first+n) of gz_path in batches of whole chunks of at most batch_bytes of text
- * (0 = 1 GiB; a single larger chunk is its own batch).  Each batch is pread (`threads` readers)
+ * (0 = 1 GiB; a single larger chunk is its own batch).  Up to five batches are in flight, each in a
+ * slot sized once at open for the largest batch: per slot ~1.13 x batch text + its compressed bytes
+ * of pinned host memory and ~1.4-2.4 x that text of HBM (8 GiB batches: ~55 GB pinned in all); the
+ * slot count drops (to 2 at least) where that would exceed half the available host memory or 80%
+ * of the free HBM.  Each batch is pread (`threads` readers)
  * into pinned memory, decoded on the GPU and handed back as host memory: the chunks' raw bytes
  * raw_k = offset_k ++ chunk_k (Parsing.cs's CombinedMemory) concatenated in `text` at raw_off[k],
  * and the records of chunk k as desc[4*j .. 4*j+3] for j in [rec_off[k], rec_off[k+1]), each the

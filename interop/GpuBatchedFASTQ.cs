@@ -83,9 +83,11 @@ public sealed class GpuBatchedFASTQ : IEnumerable<FastqRecord>, IDisposable
     private readonly int _Threads;
     private readonly GpuJob? _Job;
 
-    /// <summary>Text per streamed batch (ppg_cursor keeps four batches in flight in pinned host
-    /// memory).  Any size: each chunk is copied into its own managed array (a chunk is below 2^31
-    /// bytes, ppg_index_validate), so a batch may exceed a managed array's limit.</summary>
+    /// <summary>Text per streamed batch.  ppg_cursor keeps up to five batches in flight, each slot
+    /// ~1.13 x BatchBytes + its compressed bytes of pinned host memory (4 GiB: ~28 GB in all; the
+    /// library drops slots where that exceeds half the available memory).  Any size: each chunk is
+    /// copied into its own managed array (a chunk is below 2^31 bytes, ppg_index_validate), so a
+    /// batch may exceed a managed array's limit.</summary>
     public long BatchBytes
     {
         get => _BatchBytes;

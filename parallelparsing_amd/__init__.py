@@ -710,7 +710,8 @@ class BatchedFASTQ:
     canonical order: chunk 0's records, then chunk 1's, ...  enable_ssd_optimization is accepted
     for signature parity (it selected 1 or 8 FileStreams, LazyFileReader.cs:27-33)."""
 
-    def __init__(self, index, gzip_path, enable_ssd_optimization=False, device=None, rank=None, world=None):
+    def __init__(self, index, gzip_path, enable_ssd_optimization=False, device=None, rank=None, world=None,
+                 comm=None):
         if isinstance(index, (str, os.PathLike)):
             index = IndexIO.Deserialize(index)
         self.index = index
@@ -721,6 +722,11 @@ class BatchedFASTQ:
         # one rank of a multi-GPU job (the reference's Task.Run fan-out, BatchedFASTQ.cs:62-77, on
         # GPUs): iteration yields this rank's share -- the contiguous chunk range ppg_partition
         # gives it -- so the ranks' records, concatenated in rank order, are the file's
+        # comm (a Comm of this job): Count() decodes only this rank's share and gathers every rank's
+        # counts (ppg_dist_decompress_all), as the C# GpuBatchedFASTQ(..., GpuJob) does
+        self.comm = comm
+        if comm is not None and world is None:
+            rank, world = comm.rank_size()
         self.rank, self.world = rank, world
         if (rank is None) != (world is None) or (world is not None and not 0 <= rank < world):
             raise ValueError("rank and world go together, 0 <= rank < world")
@@ -749,11 +755,20 @@ class BatchedFASTQ:
         streamed from the file, nothing materialised on the host."""
         if self._shard is not None:
             return self._shard.total_records
+        if self.world is not None:
+            # one rank of a job: its own share decoded, the counts gathered -- every rank returns the
+            # whole file's total (never each rank decoding the whole file, ADVICE r03)
+            if self.comm is None:
+                raise ValueError("Count() of a rank's BatchedFASTQ needs the job's comm (BatchedFASTQ(..., comm=))")
+            _, _, total = dist_decompress_all(self.index, self.gzip_path, self.comm, device=self.dev)
+            return total
         _, total, _ = decompress_file(self.index, self.gzip_path, device=self.dev,
                                       threads=16 if self.enable_ssd_optimization else 8)
         return total
 
-    batch_bytes = 1 << 30   # text per streamed batch (ppg_cursor): host memory stays ~2x this
+    # text per streamed batch (ppg_cursor): up to five batches in flight, each ~1.13x this + its
+    # compressed bytes of pinned host memory (ppg_cursor_open caps the slots by available memory)
+    batch_bytes = 1 << 30
 
     def __iter__(self):
         """Records streamed through ppg_cursor in bounded memory, canonical chunk order; each

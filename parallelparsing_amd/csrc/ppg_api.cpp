@@ -694,7 +694,9 @@ int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms) {
     if ((size_t)(r0 + 4 * tot) > sh->recs.n) {
         // grow, keeping the earlier batches' descriptors, and write this batch's again
         DevBuf<uint32_t> grown;
-        HIPCHK(grown.alloc((size_t)(r0 + 4 * tot + (r0 + 4 * tot) / 8 + 4096)));
+        // half again what is needed: a shard whose records average under 256 B grows O(log) times,
+        // not once per batch (each growth copies every earlier batch's descriptors)
+        HIPCHK(grown.alloc((size_t)(r0 + 4 * tot + (r0 + 4 * tot) / 2 + 4096)));
         if (r0) HIPCHK(hipMemcpyAsync(grown.p, sh->recs.p, 4 * r0, hipMemcpyDeviceToDevice, s));
         std::swap(grown.p, sh->recs.p);
         std::swap(grown.n, sh->recs.n);

@@ -58,6 +58,18 @@ struct Slot {
 
 }  // namespace
 
+// MemAvailable of /proc/meminfo in bytes (page cache included: it is reclaimable), or 0
+static double host_mem_available() {
+    FILE *f = fopen("/proc/meminfo", "r");
+    if (!f) return 0;
+    char line[256];
+    double kb = 0;
+    while (fgets(line, sizeof line, f))
+        if (sscanf(line, "MemAvailable: %lf kB", &kb) == 1) break;
+    fclose(f);
+    return kb * 1024.0;
+}
+
 struct ppg_cursor {
     ppg_ctx *ctx = nullptr;
     const ppg_index *ix = nullptr;
@@ -134,6 +146,18 @@ struct ppg_cursor {
             cmax = std::max(cmax, comp_len(i));
             rmax = std::max(rmax, raw_len(i));
         }
+        // every slot holds its largest batch pinned on the host (compressed bytes, raw text,
+        // descriptors) and on the device (the same + the shard's output, census and records):
+        // fewer slots (not below 2) when they would take more than half the available host memory
+        // or 80% of the free device memory (at 4 GiB batches, 5 slots are ~28 GB pinned)
+        const double host_slot = (double)cmax + (double)rmax * 1.125;
+        const double dev_slot = (double)cmax + (double)rmax * (pack == 1 ? 2.4 : 1.4);
+        size_t dfree = 0, dtotal = 0;
+        const double havail = host_mem_available();
+        if (hipMemGetInfo(&dfree, &dtotal) != hipSuccess) dfree = 0;
+        while (nslots > 2 && ((havail > 0 && nslots * host_slot > 0.5 * havail) ||
+                              (dfree > 0 && nslots * dev_slot > 0.8 * (double)dfree)))
+            nslots--;
         for (int q = 0; q < nslots; q++) {
             Slot &s = slot[q];
             HIPCHK(s.pcomp.alloc((size_t)cmax));
@@ -249,7 +273,7 @@ int ppg_cursor_open(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int3
     if (!ctx || !ix || !gz_path || !out || first < 0 || n < 0 || (size_t)first + (size_t)n + 1 > ix->pts.size())
         return PPG_ARG_ERROR;
     if (int v = ppg_index_validate(ix, first, n)) return v;
-    if (batch_bytes <= 0) batch_bytes = (int64_t)4 << 30;
+    if (batch_bytes <= 0) batch_bytes = (int64_t)1 << 30;   // callers wanting throughput ask for more (bench: 8 GiB)
     HIPCHK(hipSetDevice(ctx->device));
     auto c = std::make_unique<ppg_cursor>();
     c->ctx = ctx;

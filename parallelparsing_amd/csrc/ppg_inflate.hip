@@ -110,6 +110,9 @@ struct Reader {
     uint32_t wi;            // next word to append to bb
     uint64_t bb;            // bit buffer, LSB = next bit
     uint32_t bn;            // valid bits in bb
+#ifdef PPG_R4_SGB
+    uint32_t sgb;           // (sg + 1) << 10: the first stream bit past the segment the decoder is in
+#endif
 };
 
 // global_load_lds_dword as inline asm: with the builtin the compiler waits for the DMA (vmcnt) before
@@ -139,6 +142,9 @@ __device__ __forceinline__ void st_enter(Reader &r, uint32_t *stream, uint32_t g
     }
     st_issue(r, stream, g + 2, lane);
     r.sg = g;
+#ifdef PPG_R4_SGB
+    r.sgb = (g + 1) << 10;
+#endif
     asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
 }
 
@@ -546,6 +552,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
     const uint64_t w0abs = (J.bit_start >> 5) & ~127ull;
     Reader r;
     r.sg = 0x7FFFFFF0u;   // nothing resident: the first seek loads
+#ifdef PPG_R4_SGB
+    r.sgb = 0;
+#endif
     r.base = comp + w0abs;
     r.nw = (uint32_t)min(nwords > w0abs ? nwords - w0abs : 1ull, 0xFFFFFFFFull);
     const uint32_t bit_limit = (uint32_t)min(J.bit_limit - w0abs * 32, 0xFFFFFFFFull);   // < 2^32 - 2^12: ppg_index_validate
@@ -605,6 +614,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
 
     while (pos < len && !last) {
         r.sg = uni(r.sg);
+#ifdef PPG_R4_SGB
+        r.sgb = uni(r.sgb);
+#endif
         r.wi = uni(r.wi);
         r.bb = uni64(r.bb);
         r.bn = uni(r.bn);
@@ -710,6 +722,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
         // through the outer loop), so the token rounds keep it in SGPRs with scalar branches
         r.sg = uni(r.sg);
+#ifdef PPG_R4_SGB
+        r.sgb = uni(r.sgb);
+#endif
         r.wi = uni(r.wi);
         r.bb = uni64(r.bb);
         r.bn = uni(r.bn);
@@ -812,13 +827,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
           // the token rounds as an inner loop with ONE latch (not special, output left): the two
           // exits of the plain form made the compiler merge them through an exit-selector register
           bool spec_ = false;
+#ifdef PPG_R4_LIM
+          // one compare per round leaves the rounds for all three reasons: a flush boundary, the end
+          // of the output, a special token (whose limit is 0)
+          const uint32_t lim = min(len, fl_next);
+          uint32_t lim_r;
+#endif
           do {
             // ---- one round: decode + walk, then one output byte per lane ----
             PPG_STAMP(t0);
             const Round R = decode(bp, cn, cw, pos, W);
             // the next round's stream words, read now: their LDS latency overlaps this round's
             // emit instead of opening the next round's chain of dependent LDS reads (r03)
+#ifdef PPG_R4_SGB
+            if (bp + R.adv >= r.sgb) st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+#else
             st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+#endif
             W = words(bp + R.adv);
 #ifdef PPG_STAMPS
             const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
@@ -918,11 +943,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
                 cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
             }
             pos += rout;
+#ifndef PPG_R4_LIM
             if (pos >= fl_next) {
                 flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
             }
+#endif
             bp += R.adv;
             asm volatile("s_setprio 0");
             if constexpr (IX) {   // past the member, or runaway output (a false start)
@@ -933,8 +960,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
             st_w0 = 0;
 #endif
             spec_ = R.spec;
+#ifdef PPG_R4_LIM
+            lim_r = spec_ ? 0u : lim;
+          } while (pos < lim_r);
+            if constexpr (IX) {
+                if (status != ST_OK) break;
+            }
+            if (pos >= fl_next) {
+                flush(fl_done, fl_next);
+                fl_done = fl_next;
+                fl_next += UNIT;
+            }
+            if (!spec_) {
+                if (pos < len) continue;   // a flush boundary: more rounds
+                break;
+            }
+#else
           } while (!spec_ && pos < len);
             if (!spec_) break;
+#endif
 
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
             asm volatile("s_setprio 2");

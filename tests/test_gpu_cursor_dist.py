@@ -163,8 +163,10 @@ def _rank(rank, world, name, path, chunksize, q):
         sh = pp2.Shard(ix, comp, a, b - a, device=dev).run()
         c1, b1, t1 = pp2.gather_counts(sh, comm, bounds)
         c2, b2, t2 = pp2.dist_decompress_all(ix, path, comm, device=dev)
+        # a rank's BatchedFASTQ.Count(): its own share decoded, every rank's counts gathered
+        t3 = pp2.BatchedFASTQ(ix, path, device=dev, comm=comm).Count()
         comm.close()
-        q.put((rank, c1.tolist(), b1.tolist(), t1, c2.tolist(), b2.tolist(), t2, bounds.tolist()))
+        q.put((rank, c1.tolist(), b1.tolist(), t1, c2.tolist(), b2.tolist(), t2 if t3 == t2 else -1, bounds.tolist()))
     except Exception as e:   # noqa: BLE001 - reported to the parent
         q.put((rank, repr(e)))
 

@@ -210,3 +210,13 @@ def test_status_class_lists_the_library_codes():
     body = body[:body.index("}")]
     vals = {int(v) for v in re.findall(r"=\s*(-\d+);", body)}
     assert vals == {v for v in _c_status_codes().values() if v <= -50}
+
+
+def test_paired_surface_uses_declared_externs():
+    """interop/GpuPairedFASTQ.cs: the pair check and the pair-number map come
+    from the C ABI (ppg_pairs_*), nothing else than PpGpu.cs declares."""
+    cs = _cs_decls()
+    used = set(re.findall(r"PpGpu\.(ppg_\w+)", _read("interop", "GpuPairedFASTQ.cs")))
+    assert {"ppg_pairs_create", "ppg_pairs_check", "ppg_pairs_records", "ppg_pairs_free", "ppg_shard_create",
+            "ppg_shard_run", "ppg_shard_copy_records", "ppg_shard_record_base"} <= used
+    assert used <= set(cs)
