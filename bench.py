@@ -205,6 +205,29 @@ def pmc_traffic(workload, build, path=None):
     return t.get("hbm_bytes_per_launch")
 
 
+def issue_roofline(build, path=None):
+    """The inflate kernel's issue-side bounds from the committed rocprofv3 stall passes of this same
+    build (profiles/inflate_stalls.json, tools/pmc_stalls.sh + tools/stall_summary.py; pinned to
+    ppg_version + ppg_build_id as traffic.json is), or None: SALU instructions per CU-cycle (the CU's
+    one scalar unit issues at most one per cycle), the VALU pipe's busy share (a wave64 VALU op
+    occupies a SIMD-32 for two cycles, MI355X_MICROARCH.md), and the wave-cycle split."""
+    path = path or os.path.join(ROOT, "profiles", "inflate_stalls.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("build") != build:
+        return None
+    c = t["counters"]
+    cyc = c["GRBM_GUI_ACTIVE"] / 8          # GRBM_GUI_ACTIVE sums the 8 XCDs
+    cus, simds = 256, 1024
+    return {"salu_per_cu_cycle": c["SQ_INSTS_SALU"] / (cus * cyc), "salu_peak_per_cu_cycle": 1.0,
+            "valu_busy": 2 * c["SQ_INSTS_VALU"] / (simds * cyc),
+            "wave_cycles": t.get("wave_cycle_split"), "source": os.path.relpath(path, ROOT),
+            "workload": t.get("workload")}
+
+
 def pcie_d2h_GBps(dev, gib=4):
     """Device -> pinned host copy rate of this box (the bound of any leg that lands decompressed
     text in host memory): one 4 GiB hipMemcpy, best of three."""
@@ -927,6 +950,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(workload, build),
                      "kernel": "ppg_inflate_kernel", "alg_bytes_per_launch": alg_local / shard.batches,
+                     "issue": issue_roofline(build),
                      "mean_launch_ms": mean_launch_s * 1e3,
                      # memory-side bytes (2 x FETCH_SIZE + WRITE_SIZE, calibrated, Infinity-Cache hits
                      # included) over the same launch time: how much of the HBM peak the traffic is

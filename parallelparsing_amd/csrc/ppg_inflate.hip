@@ -746,7 +746,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
         // decode of the round starting at output position pos, stream bit bp, carry (cn, cw):
         // returns the token words placed at their output offsets, the output bytes the round's
         // tokens cover (off), the bit advance (adv) and whether it stopped at a special token
-        struct Round { uint32_t vtin, off, adv; bool spec; };
+#ifdef PPG_R4_ISPEC
+        using SpecT = uint32_t;   // 128 for a special token: an integer the compiler keeps in one SGPR
+#else
+        using SpecT = bool;
+#endif
+        struct Round { uint32_t vtin, off, adv; SpecT spec; };
         // the five stream words a lane decodes from at bit bp (st_enter made their segments resident)
         struct Words { uint32_t x0, x1, x2, x3, x4; };
         auto words = [&](uint32_t bp) -> Words {
@@ -754,12 +759,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
             const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
             return Words{sw[0], sw[1], sw[2], sw[3], sw[4]};
         };
+#ifdef PPG_R4_HOT
+        auto decode = [&](auto hot, uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos, const Words &W) -> Round {
+            constexpr bool HOT = decltype(hot)::value;
+#else
         auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos, const Words &W) -> Round {
+            constexpr bool HOT = false;
+#endif
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t vtin = 0;
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
-            bool spec = false;
-            if (off < min(64u, len - pos)) {
+            SpecT spec = 0;
+            if (off < (HOT ? 64u : min(64u, len - pos))) {
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring, read during the previous round's emit)
                 const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
@@ -785,7 +796,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
 #ifdef PPG_STAMPS
                 st_w0 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(vta ^ vtb);
 #endif
-                if (len - pos >= 64) {
+                if (HOT || len - pos >= 64) {
                     X = off << 8;
                     asm volatile("s_setprio 2");
                     walk_asm(vta, vtin, X);
@@ -815,7 +826,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
                     }
                     off = ((X >> 8) & 511u) - cl;
                 }
-                spec = (X & 128u) != 0u;
+                spec = (SpecT)(X & 128u);
                 s = half + (X & 127u);   // bit offset of the next token (of the special one: bit 7 dropped)
             }
             return Round{vtin, off, s, spec};
@@ -823,20 +834,175 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
 
         st_enter(r, S.stream, bp >> 10, lane);
         Words W = words(bp);
+#ifdef PPG_R4_HOT
+        // one round (decode + walk, one output byte per lane); HOT: at least 322 output bytes are left
+        // (a round's tokens cover at most 63 + 258), so neither the walk's stop nor the emitted bytes
+        // need the chunk's end -- the rounds of the chunk's last 322 bytes run the general form
+        auto one_round = [&](auto hot) -> SpecT {
+            constexpr bool HOT = decltype(hot)::value;
+            PPG_STAMP(t0);
+            const Round R = decode(hot, bp, cn, cw, pos, W);
+            // the next round's stream words, read now: their LDS latency overlaps this round's
+            // emit instead of opening the next round's chain of dependent LDS reads (r03)
+#ifdef PPG_R4_SGB
+            if (bp + R.adv >= r.sgb) st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+#else
+            st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+#endif
+            W = words(bp + R.adv);
+#ifdef PPG_STAMPS
+            const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
+            if (st_w0 < t0) st_w0 = t1;   // no walk this round
+            sa_dec += st_w0 - t0;
+            sa_walk += t1 - st_w0;
+            sa_rounds++;
+#endif
+#ifdef PPG_STATS
+            st_rounds++;
+            st_tokens += (uint32_t)__popcll(__ballot(R.vtin != 0));
+            if (R.spec) st_spec++;
+            if (R.off < 64) st_short++;
+#endif
+            const uint32_t tot = HOT ? R.off : min(R.off, len - pos);   // output bytes of the round's tokens
+            const uint32_t rout = min(tot, 64u);          // ... emitted this round
+            const uint64_t mo = __ballot(R.vtin != 0);    // token start offsets (never 0 words)
+            // All 64 lanes write: lanes past rout leave garbage in the slots of positions
+            // [pos + rout, pos + 64), which later rounds overwrite before use; the slots' previous
+            // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
+            // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
+            {
+                // 4 * (63 - clz) in one v_mad_i32_i24 (the compiler's form: shift + xor)
+                uint32_t sj4;
+                asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
+                const uint32_t inf = bperm(sj4, R.vtin);
+                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
+                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                uint32_t val;   // (IX: a literal is the symbol 0x8000 | byte; written apart, the DecompressAll
+                                // instance's code is unchanged -- the folded "| 0" moved its schedule)
+                if constexpr (IX) val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
+                else val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
+                const uint64_t fm = __ballot(far);
+#ifdef PPG_STATS
+                if (fm) st_far++;
+#endif
+#ifdef PPG_STAMPS
+                const uint64_t t2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
+                sa_rd += t2 - t1;
+#endif
+                if (fm) {
+                    // older than the ring: the flushed output (this wave's own earlier stores), as
+                    // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
+                    // juggling); references into the Point's window (first 32 KiB only) separately
+                    const int32_t p = (int32_t)pos + jj;
+                    const bool fo = far && p >= 0;
+                    if constexpr (IX) {
+                        const uint32_t q = 2u * ((uint32_t)p & IX_RING_MASK);
+                        const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
+                        val = fo ? __builtin_amdgcn_ubfe(w, q << 3, 16u) : val;
+                    } else {
+                        // one byte load at ob + oa + p (pos + oa is wave-uniform)
+                        const uint32_t b = far_load_u8(ob, fo ? (uint32_t)jj + (pos + oa) : 0u);
+                        val = fo ? b : val;
+                    }
+                    const bool fd = far && p < 0;
+                    const uint64_t dm = fm & __ballot(p < 0);   // (a ballot of fd itself went through two VALU)
+                    if (dm) {   // rare: the chunk's first 32 KiB
+                        uint32_t db;
+                        if constexpr (IX) db = 32768u + (uint32_t)p;          // the history symbol itself
+                        else db = dict[fd ? 32768u + (uint32_t)p : 0u];       // p >= -32768
+                        val = fd ? db : val;
+                    }
+                }
+#ifdef PPG_STAMPS
+                const uint64_t t3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
+                sa_far += t3 - t2;
+                sa_farr += fm ? 1 : 0;
+#endif
+                const bool dep = jj >= 0;                             // produced in this round
+                if (__ballot(dep)) {
+                    // chains inside the round (short distances): pointer doubling to a resolved byte
+                    int32_t ptr = dep ? jj : lane;
+#ifdef PPG_STATS
+                    st_dep++;
+#endif
+                    for (;;) {
+#ifdef PPG_STATS
+                        st_dbl++;
+#endif
+                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
+                        if (!__ballot(p2 != ptr)) break;
+                        ptr = p2;
+                    }
+                    val = bperm((uint32_t)ptr << 2, val);
+                }
+                S.ring[(rb0 + pos + lane) & RM] = (RingT)val;
+#ifdef PPG_STAMPS
+                const uint64_t t4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
+                sa_dep += t4 - t3;
+                st_w0 = t4;   // reused below: start of the round's tail
+#endif
+            }
+            cn = tot - rout;
+            if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
+                cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
+            }
+            pos += rout;
+#ifndef PPG_R4_LIM
+            if (pos >= fl_next) {
+                flush(fl_done, fl_next);
+                fl_done = fl_next;
+                fl_next += UNIT;
+            }
+#endif
+            bp += R.adv;
+            asm volatile("s_setprio 0");
+            if constexpr (IX) {   // past the member, or runaway output (a false start)
+                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; return true; }
+            }
+#ifdef PPG_STAMPS
+            sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
+            st_w0 = 0;
+#endif
+            return R.spec;
+        };
+#endif
         for (;;) {
           // the token rounds as an inner loop with ONE latch (not special, output left): the two
           // exits of the plain form made the compiler merge them through an exit-selector register
-          bool spec_ = false;
+          SpecT spec_ = 0;
 #ifdef PPG_R4_LIM
           // one compare per round leaves the rounds for all three reasons: a flush boundary, the end
           // of the output, a special token (whose limit is 0)
           const uint32_t lim = min(len, fl_next);
           uint32_t lim_r;
 #endif
+#ifdef PPG_R4_HOT
+          {
+              const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
+              if (pos < limh) {
+                  do {
+                      spec_ = one_round(std::true_type{});
+                      lim_r = spec_ ? 0u : limh;
+                  } while (pos < lim_r);
+              }
+              if (!spec_ && pos < lim) {
+                  do {
+                      spec_ = one_round(std::false_type{});
+                      lim_r = spec_ ? 0u : lim;
+                  } while (pos < lim_r);
+              }
+          }
+          if (false)
+#endif
           do {
             // ---- one round: decode + walk, then one output byte per lane ----
             PPG_STAMP(t0);
+#ifdef PPG_R4_HOT
+            const Round R = decode(std::false_type{}, bp, cn, cw, pos, W);
+#else
             const Round R = decode(bp, cn, cw, pos, W);
+#endif
             // the next round's stream words, read now: their LDS latency overlaps this round's
             // emit instead of opening the next round's chain of dependent LDS reads (r03)
 #ifdef PPG_R4_SGB

@@ -41,3 +41,16 @@ def test_stale_build_is_refused(tmp_path):
 
 def test_other_workload_is_refused(tmp_path):
     assert bench.pmc_traffic("configs[1]: 1 M-read .fastq.gz, chunk=10000", pp.build_info(), _write(tmp_path)) is None
+
+
+def test_issue_roofline_only_for_the_same_build(tmp_path):
+    """roofline.issue: SALU per CU-cycle and VALU busy from the committed stall
+    passes, quoted only for the build they measured."""
+    b = {"ppg_version": "v", "build_id": "inflate-aaaa"}
+    c = {"GRBM_GUI_ACTIVE": 8 * 1.0e9, "SQ_INSTS_SALU": 0.5 * 256 * 1.0e9, "SQ_INSTS_VALU": 0.25 * 1024 * 1.0e9}
+    p = tmp_path / "stalls.json"
+    p.write_text(json.dumps({"build": b, "counters": c, "workload": "w", "wave_cycle_split": {}}))
+    r = bench.issue_roofline(b, str(p))
+    assert abs(r["salu_per_cu_cycle"] - 0.5) < 1e-9 and abs(r["valu_busy"] - 0.5) < 1e-9
+    assert bench.issue_roofline({"ppg_version": "v", "build_id": "inflate-bbbb"}, str(p)) is None
+    assert bench.issue_roofline(b, str(tmp_path / "missing.json")) is None

@@ -67,8 +67,19 @@ def main(tag):
         out["probes_inflate_ms_50gb_step"] = probes
         out["probes_note"] = ("same box, tools/ab_bench.sh: nostore = no output stores (far bytes read garbage), "
                               "nofar = far bytes read from the ring: timing probes only, wrong output")
+    # the build the passes measured (the bench's JSON line in a pass's log): bench.py quotes these
+    # counters (roofline.issue) only for the same ppg_version + ppg_build_id
+    for g in "ABCDE":
+        p = os.path.join(G, f"stall_{g}.log")
+        if os.path.exists(p):
+            ln = [x for x in open(p) if x.startswith("{")]
+            if ln:
+                out["build"] = json.loads(ln[-1]).get("build")
+                break
     path = os.path.join(ROOT, "profiles", f"{tag}_inflate_stalls.json")
     json.dump(out, open(path, "w"), indent=1)
+    if out.get("build"):
+        json.dump(out, open(os.path.join(ROOT, "profiles", "inflate_stalls.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
