@@ -315,8 +315,10 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
     """README "Decompress" (ppg_decompress_chunk, thread safe): T host threads calling it on one ctx,
     each for its own chunk at a time, as the reference's one task per chunk does
     (BatchedFASTQ.cs:62-77).  Slices from host memory, bytes + descriptors back into host buffers;
-    the per-chunk record counts are checked against the timed DecompressAll run's.  Twice: with the
-    plain index (one wave per chunk) and with side points attached (up to `side` waves per chunk)."""
+    the per-chunk record counts are checked against the timed DecompressAll run's.  Three ways: the
+    plain index (launches of <= 256 chunks find each chunk's inner block starts on the GPU and decode
+    it as up to 16 waves), the same with that search off (PPG_CHUNK_NO_FIND: one wave per chunk), and
+    with the index's own side points attached (up to `side` waves per chunk)."""
     import threading
     import parallelparsing_amd as pp
     nmax = min(max_chunks, len(counts), per_thread * max(threads_list))
@@ -359,15 +361,26 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
         calls, launches = after["calls"] - before["calls"], after["launches"] - before["launches"]
         return {"chunks": n, "records_per_s": float(got.sum()) / sec, "chunks_per_s": n / sec,
                 "ms_per_call": sec * 1e3 * T / n, "seconds": sec, "launches": launches,
-                "chunks_per_launch": calls / max(1, launches)}
+                "chunks_per_launch": calls / max(1, launches),
+                "split_chunks": after["split_chunks"] - before["split_chunks"],
+                "found_side_points": after["side_points"] - before["side_points"]}
+
+    def no_find(T):
+        os.environ["PPG_CHUNK_NO_FIND"] = "1"
+        try:
+            return leg(plain, T)
+        finally:
+            os.environ.pop("PPG_CHUNK_NO_FIND", None)
 
     leg(plain, 8)   # warm: the slots' buffers grow to their working size
     out = {f"T{T}": leg(plain, T) for T in threads_list}
+    out["no_find"] = {f"T{T}": no_find(T) for T in threads_list}
     out["side_points"] = {f"T{T}": leg(split, T) for T in threads_list}
     out["note"] = ("ppg_decompress_chunk from T host threads on one ctx (concurrent calls combined into shared "
-                   "launches, two launch slots); plain index: one wave per chunk; side_points: the same chunks with "
-                   f"<= {side} waves each (ppg_index_set_side_points); host slices in, bytes + descriptors out; not "
-                   "the bench value")
+                   "launches, two launch slots); plain index: each chunk's inner block starts found on the GPU "
+                   "(<= 16 waves per chunk); no_find: one wave per chunk; side_points: the index's own, "
+                   f"<= {side} waves per chunk (ppg_index_set_side_points); host slices in, bytes + descriptors out; "
+                   "not the bench value")
     return out
 
 

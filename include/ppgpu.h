@@ -148,13 +148,19 @@ int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream);
  * Thread safe (README.md:38-50): concurrent calls on one ctx are combined into shared launches (two
  * launch slots, each with its own stream and buffers that only grow: no hipMalloc/hipFree per call
  * once warm); every call gets its own chunk's results.  A chunk of an index with side points
- * (ppg_index_build_gpu_side) is decoded as one wave per piece. */
+ * (ppg_index_build_gpu_side) is decoded as one wave per piece; in a launch of at most 256 chunks,
+ * a chunk of an index without them gets its inner block starts found on the GPU first (candidate
+ * block headers, a speculative symbolic decode, the verified chain of block ends from the chunk's
+ * Point and their resolved 32 KiB histories -- CreateIndex's own kernels) and is decoded as up to
+ * 16 pieces too.  Environment PPG_CHUNK_NO_FIND=1 turns the search off. */
 int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
                          uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
                          int64_t *nrec);
 /* ppg_decompress_chunk calls on this ctx so far, the launches that served them, the most calls one
  * launch served. */
 int ppg_decompress_chunk_stats(ppg_ctx *ctx, int64_t *calls, int64_t *launches, int64_t *max_batch);
+/* Chunks split by the search for inner block starts above, and the side points it found. */
+int ppg_decompress_chunk_split_stats(ppg_ctx *ctx, int64_t *chunks, int64_t *side_points);
 
 /* ======================= DecompressAll over a shard (README "DecompressAll") =======================
  * A shard is chunks [first, first+n) of an index, with their compressed bytes resident on the

@@ -99,6 +99,8 @@ internal static unsafe class PpGpu
         long sliceLen, byte* output, long outCap, out long produced, uint* recs, long recCap, out long nrec);
     [DllImport(Lib)] public static extern int ppg_decompress_chunk_stats(nint ctx, out long calls, out long launches,
         out long maxBatch);
+    [DllImport(Lib)] public static extern int ppg_decompress_chunk_split_stats(nint ctx, out long chunks,
+        out long sidePoints);
 
     // ---- README "DecompressAll": a shard of chunks resident on one GPU ----
     [DllImport(Lib)] public static extern int ppg_shard_create(nint ctx, nint ix, int first, int n, byte* comp,

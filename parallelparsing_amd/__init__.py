@@ -193,11 +193,14 @@ class Device:
         check(lib.ppg_stream_wait_ctx(self._h, C.c_void_p(_stream_handle(stream))), "ppg_stream_wait_ctx")
 
     def decompress_chunk_stats(self):
-        """{calls, launches, max_batch} of ppg_decompress_chunk on this ctx: how the thread-safe
-        per-chunk Decompress combined concurrent calls into launches."""
-        v = [C.c_int64() for _ in range(3)]
-        check(lib.ppg_decompress_chunk_stats(self._h, *[C.byref(x) for x in v]), "ppg_decompress_chunk_stats")
-        return dict(zip(("calls", "launches", "max_batch"), (x.value for x in v)))
+        """{calls, launches, max_batch, split_chunks, side_points} of ppg_decompress_chunk on this
+        ctx: how the thread-safe per-chunk Decompress combined concurrent calls into launches, and
+        how many chunks it split at inner block starts it found on the GPU."""
+        v = [C.c_int64() for _ in range(5)]
+        check(lib.ppg_decompress_chunk_stats(self._h, *[C.byref(x) for x in v[:3]]), "ppg_decompress_chunk_stats")
+        check(lib.ppg_decompress_chunk_split_stats(self._h, *[C.byref(x) for x in v[3:]]),
+              "ppg_decompress_chunk_split_stats")
+        return dict(zip(("calls", "launches", "max_batch", "split_chunks", "side_points"), (x.value for x in v)))
 
     def after_torch(self):
         """wait_stream(torch's current stream on this device): call before a ppg call reads device

@@ -91,6 +91,7 @@ _SIGS = {
     "ppg_stream_wait_ctx": (C.c_int, [vp, vp]),
     "ppg_decompress_chunk": (C.c_int, [vp, vp, i32, vp, i64, vp, i64, P(i64), vp, i64, P(i64)]),
     "ppg_decompress_chunk_stats": (C.c_int, [vp, P(i64), P(i64), P(i64)]),
+    "ppg_decompress_chunk_split_stats": (C.c_int, [vp, P(i64), P(i64)]),
     "ppg_shard_create": (C.c_int, [vp, vp, i32, i32, vp, i64, C.c_int, i64, P(vp)]),
     "ppg_shard_free": (None, [vp]),
     "ppg_shard_run": (C.c_int, [vp]),

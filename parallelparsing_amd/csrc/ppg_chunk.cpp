@@ -18,13 +18,27 @@
 // Chunks whose index carries side points (ppg_index_build_gpu_side) are decoded as one wave per
 // piece between their inner block starts (ppg_shard_set_split), exactly as DecompressAll does.
 #include "ppg_host.h"
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
 
+hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
+                                 const uint64_t *hi, uint64_t *cand, int n);
+hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
+                                 const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
+                                 int njobs);
+hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
+                             const uint8_t *ref, uint32_t *diff, int n);
+hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
+                              uint8_t *W, uint16_t *M);
+int ppg_resolve_groups(int np);
+
 namespace {
 
 constexpr int kChunkSlots = 2;
+constexpr uint64_t kPieceRing = 65536;     // CreateIndex pass 1's symbolic output ring per piece (IX_RING_BYTES)
+constexpr int kFindMaxChunks = 256;        // launches of more chunks fill the GPU by themselves
 constexpr size_t kSliceAlign = 64;   // each gathered slice starts on its own 64-B line
 
 struct ChunkReq {
@@ -49,12 +63,25 @@ hipError_t grow_buf(B &b, size_t need) {
     return b.alloc(std::max(need, b.n + b.n / 2));
 }
 
+// device scratch of find_side_points (grow only)
+struct FindScratch {
+    DevBuf<uint64_t> lo, hi, cand;
+    DevBuf<PpgInflateJob> jobs;
+    DevBuf<PpgInflateResult> res;
+    DevBuf<PpgBlockEnd> blk;
+    DevBuf<uint8_t> ring, ta, ident, W;
+    DevBuf<PpgGather> gat;
+    DevBuf<uint32_t> slots;
+    DevBuf<uint16_t> maps;
+};
+
 struct ChunkSlot {
     hipStream_t s = nullptr;
     ppg_shard *sh = nullptr;
     PinnedBuf in;                       // the launch's slices, gathered
     DevBuf<uint8_t> comp;
     PinnedBuf res;                      // outputs, then descriptors
+    FindScratch fs;
     bool busy = false;
     int readers = 0;                    // callers still copying out of `res`
 };
@@ -67,6 +94,7 @@ struct ChunkService {
     std::deque<ChunkReq *> pending;
     ChunkSlot slot[kChunkSlots];
     int64_t calls = 0, launches = 0, max_batch = 0;
+    std::atomic<int64_t> found_chunks{0}, found_points{0};   // find_side_points' splits
 };
 
 ChunkService *chunk_service_new() { return new ChunkService; }
@@ -100,9 +128,167 @@ void side_points_of(const ppg_index *ix, int32_t k, uint64_t job_bit, int64_t ou
     }
 }
 
+// Side points for chunks whose index has none (a .gzi carries only the Points): the inner deflate
+// block starts of each chunk found on the GPU the way the GPU CreateIndex finds them
+// (ppg_index_gpu.cpp) -- candidate dynamic-block headers every ~1/16 of the chunk's compressed bytes
+// (ppg_block_find_kernel), each piece but the last decoded with symbolic output until a block ends
+// at or past the next candidate (the inflate kernel's IX mode, the same kernels as CreateIndex pass
+// 1), the chain of block ends walked from the chunk's own Point (a block end that is not the next
+// candidate's start ends the chain there: that end is still a real block start), and the 32 KiB
+// history at every verified block start resolved from the pieces' symbolic tails starting from the
+// Point's window (ppg_resolve_*).  A lone chunk then decodes as ~16 waves instead of one: the
+// speculative pass costs about one piece's decode, the split decode another.  Coordinates: bits in
+// the launch's gathered comp buffer, outputs in the launch's output (the shard's virtual ones).
+struct FindChunk {
+    uint64_t bit0, bit1;                // compressed bits of the chunk: [from's start bit, slice end)
+    uint64_t bit_end;                   // to's block start (8 to.Input - to.Bits), or bit1 for the last chunk
+    int64_t out0;                       // the chunk's first output byte (launch coordinates)
+    const uint8_t *window;              // the Point's 32 KiB
+};
+
+int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const std::vector<FindChunk> &ch,
+                     std::vector<int64_t> &sbit, std::vector<int64_t> &sout, ByteVec &swin, int64_t &nsplit) {
+    hipStream_t s = sl.s;
+    FindScratch &F = sl.fs;
+    // candidates: the chunk cut into up to 16 pieces of >= 48 KiB of compressed bytes
+    std::vector<uint64_t> lo, hi;
+    std::vector<size_t> cfirst(ch.size() + 1, 0);
+    for (size_t c = 0; c < ch.size(); c++) {
+        const uint64_t span = ch[c].bit1 - ch[c].bit0;
+        const uint64_t pb = std::max<uint64_t>(8ull * 48 * 1024, span / 16);
+        for (uint64_t a = ch[c].bit0 + pb; a + 8ull * 1024 < ch[c].bit1; a += pb) {
+            lo.push_back(a);
+            hi.push_back(std::min(a + pb, ch[c].bit1));
+        }
+        cfirst[c + 1] = lo.size();
+    }
+    if (lo.empty()) return PPG_OK;
+    const size_t nc = lo.size();
+    HIPCHK(grow_buf(F.lo, nc));
+    HIPCHK(grow_buf(F.hi, nc));
+    HIPCHK(grow_buf(F.cand, nc));
+    HIPCHK(hipMemcpyAsync(F.lo.p, lo.data(), 8 * nc, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(F.hi.p, hi.data(), 8 * nc, hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_block_find(s, comp, nwords, F.lo.p, F.hi.p, F.cand.p, (int)nc));
+    std::vector<uint64_t> cand(nc);
+    HIPCHK(hipMemcpyAsync(cand.data(), F.cand.p, 8 * nc, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // pieces: chunk c's Point, then its candidates; every piece but the last decoded to the next
+    struct Piece { size_t chunk; uint64_t start, stop; };
+    std::vector<Piece> pc;
+    std::vector<size_t> pfirst(ch.size() + 1, 0);
+    for (size_t c = 0; c < ch.size(); c++) {
+        std::vector<uint64_t> st{ch[c].bit0};
+        for (size_t k = cfirst[c]; k < cfirst[c + 1]; k++)
+            if (cand[k] != ~0ull && cand[k] > st.back()) st.push_back(cand[k]);
+        for (size_t j = 0; j + 1 < st.size(); j++) pc.push_back({c, st[j], st[j + 1]});
+        pfirst[c + 1] = pc.size();
+    }
+    const size_t np = pc.size();
+    if (!np) return PPG_OK;
+    std::vector<PpgInflateJob> jobs(np);
+    uint64_t nblk = 0;
+    for (size_t q = 0; q < np; q++) {
+        PpgInflateJob &J = jobs[q];
+        J = PpgInflateJob{};
+        J.bit_start = pc[q].start;
+        J.bit_limit = ch[pc[q].chunk].bit1;
+        J.out_off = (uint64_t)q * kPieceRing;
+        J.expect_end = ~0ull;
+        J.stop_bit = pc[q].stop;
+        J.blk_off = (uint32_t)nblk;
+        J.blk_cap = (uint32_t)((pc[q].stop - pc[q].start) / 8 / 2048 + 64);
+        nblk += J.blk_cap;
+    }
+    HIPCHK(grow_buf(F.jobs, np));
+    HIPCHK(grow_buf(F.res, np));
+    HIPCHK(grow_buf(F.blk, (size_t)nblk));
+    HIPCHK(grow_buf(F.ring, np * 2 * kPieceRing));
+    HIPCHK(grow_buf(F.ta, np * 2 * kWin));
+    if (!F.ident.p) {   // u16 0..32767: position p < 0 of a piece is history symbol 32768 + p
+        std::vector<uint16_t> id(kWin);
+        for (int i = 0; i < kWin; i++) id[(size_t)i] = (uint16_t)i;
+        HIPCHK(F.ident.alloc(2 * kWin));
+        HIPCHK(hipMemcpyAsync(F.ident.p, id.data(), 2 * kWin, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(F.jobs.p, jobs.data(), sizeof(PpgInflateJob) * np, hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_inflate_ix(s, comp, nwords, F.jobs.p, F.ident.p, F.ring.p, F.res.p, F.blk.p, (int)np));
+    std::vector<PpgInflateResult> res(np);
+    std::vector<PpgBlockEnd> blk((size_t)nblk);
+    HIPCHK(hipMemcpyAsync(res.data(), F.res.p, sizeof(PpgInflateResult) * np, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(blk.data(), F.blk.p, sizeof(PpgBlockEnd) * nblk, hipMemcpyDeviceToHost, s));
+    // the symbolic tails: the last 32 Ki symbols of each piece's ring, as two 32 KiB byte halves
+    std::vector<PpgGather> g(2 * np);
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t q = 0; q < np; q++) {
+        const uint64_t endb = 2 * res[q].produced;
+        g[2 * q] = PpgGather{(uint64_t)q * 2 * kPieceRing, (uint64_t)kWin, endb - kWin, 2 * kPieceRing - 1, 0};
+        g[2 * q + 1] = PpgGather{(uint64_t)q * 2 * kPieceRing, (uint64_t)kWin, endb, 2 * kPieceRing - 1, 0};
+    }
+    HIPCHK(grow_buf(F.gat, 2 * np));
+    HIPCHK(hipMemcpyAsync(F.gat.p, g.data(), sizeof(PpgGather) * 2 * np, hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_gather(s, F.ring.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * np)));
+    // the chains: piece j of a chunk is followed when its last block end is piece j+1's start
+    std::vector<std::vector<uint32_t>> chain(ch.size());
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ends(ch.size());   // (bit, chunk-relative output)
+    for (size_t c = 0; c < ch.size(); c++) {
+        uint64_t outc = 0;
+        for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) {
+            const PpgInflateResult &r = res[q];
+            const uint32_t nb = std::min(r.nblocks, jobs[q].blk_cap);
+            if (r.status != 0 || nb == 0 || r.last || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN))) break;
+            const PpgBlockEnd &B = blk[jobs[q].blk_off + nb - 1];
+            const uint64_t E = B.end_bit;
+            if (E >= ch[c].bit_end || B.out_end != r.produced) break;
+            outc += r.produced;
+            chain[c].push_back((uint32_t)q);
+            ends[c].push_back({E, outc});
+            if (q + 1 >= pfirst[c + 1] || pc[q + 1].start != E) break;   // the next candidate was false
+        }
+    }
+    // histories at the verified block ends: W[0] = the Point's window, W[j+1] = T_j(W[j])
+    size_t wmax = 0, cmax = 0;
+    for (size_t c = 0; c < ch.size(); c++) {
+        wmax = std::max(wmax, chain[c].size() + 1);
+        cmax = std::max(cmax, chain[c].size());
+    }
+    if (!cmax) return PPG_OK;
+    HIPCHK(grow_buf(F.W, ch.size() * wmax * kWin));
+    HIPCHK(grow_buf(F.slots, ch.size() * wmax));
+    HIPCHK(grow_buf(F.maps, (size_t)ppg_resolve_groups((int)cmax) * kWin));
+    std::vector<uint32_t> sl_all(ch.size() * wmax, 0);
+    for (size_t c = 0; c < ch.size(); c++)
+        std::copy(chain[c].begin(), chain[c].end(), sl_all.begin() + (ptrdiff_t)(c * wmax));
+    HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * sl_all.size(), hipMemcpyHostToDevice, s));
+    for (size_t c = 0; c < ch.size(); c++) {
+        if (chain[c].empty()) continue;
+        uint8_t *W = F.W.p + c * wmax * kWin;
+        HIPCHK(hipMemcpyAsync(W, ch[c].window, kWin, hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_resolve(s, F.ta.p, nullptr, F.slots.p + c * wmax, (int)chain[c].size(), W, F.maps.p));
+    }
+    const size_t base = sbit.size();
+    size_t nnew = 0;
+    for (size_t c = 0; c < ch.size(); c++) nnew += chain[c].size();
+    swin.resize((base + nnew) * kWin);
+    size_t t = base;
+    for (size_t c = 0; c < ch.size(); c++) {
+        if (chain[c].empty()) continue;
+        HIPCHK(hipMemcpyAsync(swin.data() + t * kWin, F.W.p + (c * wmax + 1) * kWin, chain[c].size() * kWin,
+                              hipMemcpyDeviceToHost, s));
+        nsplit++;
+        for (const auto &e : ends[c]) {
+            sbit.push_back((int64_t)e.first);
+            sout.push_back(ch[c].out0 + (int64_t)e.second);
+        }
+        t += chain[c].size();
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return PPG_OK;
+}
+
 // One launch of the requests `batch` on slot `sl` (the caller holds the slot, not the lock).  Sets
 // every request's rc and, for a decoded chunk, where its bytes and descriptors sit in sl.res.
-int run_launch(ppg_ctx *ctx, ChunkSlot &sl, std::vector<ChunkReq *> &batch) {
+int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<ChunkReq *> &batch) {
     HIPCHK(hipSetDevice(ctx->device));
     if (!sl.s) HIPCHK(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     if (!sl.sh) {
@@ -140,6 +326,7 @@ int run_launch(ppg_ctx *ctx, ChunkSlot &sl, std::vector<ChunkReq *> &batch) {
             const auto &O = r->ix->side_out;
             nsub += (size_t)std::max<std::ptrdiff_t>(0, std::lower_bound(O.begin(), O.end(), to.output) -
                                                             std::upper_bound(O.begin(), O.end(), from.output));
+            if (O.empty() && n <= (size_t)kFindMaxChunks) nsub += 16;   // find_side_points' at most
         }
         ppg_shard *sh = sl.sh;
         HIPCHK(grow_buf(sh->jobs, n));
@@ -167,11 +354,31 @@ int run_launch(ppg_ctx *ctx, ChunkSlot &sl, std::vector<ChunkReq *> &batch) {
     ppg_shard *sh = sl.sh;
     int rc = shard_prepare_specs(sh, spec.data(), (int32_t)go.size(), sl.comp.p, (int64_t)comp_len, 0, sl.s, nullptr);
     if (rc != PPG_OK) return rc;
-    {   // side points of the chunks that have them (the index's, shifted into this launch)
+    {   // side points of the chunks that have them (the index's, shifted into this launch); the
+        // others' found on the GPU when the launch is too small to fill it
         std::vector<int64_t> sbit, sout;
         ByteVec swin;
-        for (size_t i = 0; i < go.size(); i++)
-            side_points_of(go[i]->ix, go[i]->k, sh->h_jobs[i].bit_start, sh->h_pout[i], sbit, sout, swin);
+        std::vector<FindChunk> find;
+        const bool findable = go.size() <= (size_t)kFindMaxChunks && !getenv("PPG_CHUNK_NO_FIND");
+        for (size_t i = 0; i < go.size(); i++) {
+            if (!go[i]->ix->side_out.empty()) {
+                side_points_of(go[i]->ix, go[i]->k, sh->h_jobs[i].bit_start, sh->h_pout[i], sbit, sout, swin);
+            } else if (findable && sh->h_jobs[i].out_len > 0) {
+                // sorted by output with the others: flush the found ones in launch order
+                const PpgInflateJob &J = sh->h_jobs[i];
+                find.push_back(FindChunk{J.bit_start, J.bit_limit, J.expect_end != ~0ull ? J.expect_end : J.bit_limit,
+                                         sh->h_pout[i], go[i]->ix->win((size_t)go[i]->k)});
+            }
+            if (!find.empty() && (i + 1 == go.size() || !go[i + 1]->ix->side_out.empty())) {
+                const size_t before = sbit.size();
+                int64_t nsplit = 0;
+                rc = find_side_points(sl, (const uint32_t *)sl.comp.p, sh->nwords, find, sbit, sout, swin, nsplit);
+                if (rc != PPG_OK) return rc;
+                svc.found_chunks += nsplit;
+                svc.found_points += (int64_t)(sbit.size() - before);
+                find.clear();
+            }
+        }
         if (!sbit.empty()) {
             rc = ppg_shard_set_split(sh, (int32_t)sbit.size(), sbit.data(), sout.data(), swin.data());
             if (rc != PPG_OK) return rc;
@@ -235,7 +442,7 @@ int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uin
         svc->launches++;
         svc->max_batch = std::max<int64_t>(svc->max_batch, (int64_t)batch.size());
         lk.unlock();
-        const int rc = run_launch(ctx, sl, batch);
+        const int rc = run_launch(ctx, *svc, sl, batch);
         lk.lock();
         for (ChunkReq *r : batch) {
             if (rc != PPG_OK) r->rc = rc;
@@ -281,6 +488,13 @@ int ppg_decompress_chunk_stats(ppg_ctx *ctx, int64_t *calls, int64_t *launches, 
     if (calls) *calls = ctx->chunks->calls;
     if (launches) *launches = ctx->chunks->launches;
     if (max_batch) *max_batch = ctx->chunks->max_batch;
+    return PPG_OK;
+}
+
+int ppg_decompress_chunk_split_stats(ppg_ctx *ctx, int64_t *chunks, int64_t *side_points) {
+    if (!ctx || !ctx->chunks) return PPG_ARG_ERROR;
+    if (chunks) *chunks = ctx->chunks->found_chunks.load();
+    if (side_points) *side_points = ctx->chunks->found_points.load();
     return PPG_OK;
 }
 

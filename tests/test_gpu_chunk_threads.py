@@ -120,6 +120,39 @@ def test_threads_200k_records_vs_oracle(file200k):
     st = dev.decompress_chunk_stats()
     assert st["calls"] == 2 * n
     assert st["launches"] < st["calls"] and st["max_batch"] > 1, st
+    # ~190 KB of gzip per chunk: the GPU search split (nearly) every chunk at its inner block starts
+    assert st["split_chunks"] > n and st["side_points"] >= st["split_chunks"], st
+
+
+def test_lone_chunks_found_side_points_vs_oracle():
+    """Chunks of 40,000 records (~4 MB of gzip) decoded one call at a time: each launch holds one
+    chunk, whose inner block starts are found on the GPU (candidates, speculative symbolic decode,
+    the verified chain from the chunk's Point, resolved histories) -- it is decoded as ~16 waves.
+    Bytes and records equal the oracle's, and equal the one-wave decode (PPG_CHUNK_NO_FIND)."""
+    import os
+    gz = synth_gz(130_000, 11)
+    oi = O.build_index(gz, 40_000)
+    dev = pp.Device(0)
+    ix = pp.Core.BuildDeflateIndex(gz, 40_000)
+    n = ix.Count - 1
+    assert n == oi.count - 1 and n >= 3
+    before = dev.decompress_chunk_stats()
+    for k in range(n):
+        b = O.extract(gz, oi, k)
+        got, buf, rec = pp.Core.ExtractDeflateIndex(slice_of(gz, ix, k), ix, k, device=dev, with_records=True)
+        assert got == len(b) and sha(buf[:got]) == sha(b), k
+        assert np.array_equal(rec, O.parse(oi.point(k)[4], b)), k
+        os.environ["PPG_CHUNK_NO_FIND"] = "1"
+        try:
+            got2, buf2, rec2 = pp.Core.ExtractDeflateIndex(slice_of(gz, ix, k), ix, k, device=dev, with_records=True)
+        finally:
+            os.environ.pop("PPG_CHUNK_NO_FIND", None)
+        assert got2 == got and sha(buf2[:got2]) == sha(b) and np.array_equal(rec2, rec), k
+    st = dev.decompress_chunk_stats()
+    split = st["split_chunks"] - before["split_chunks"]
+    pts = st["side_points"] - before["side_points"]
+    print(f"[found] {n} chunks split, {pts} side points")
+    assert split == n and pts >= 2 * n, (split, pts)
 
 
 def test_threads_side_points_split_chunks(file200k):
