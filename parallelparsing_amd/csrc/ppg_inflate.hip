@@ -464,8 +464,8 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 // written out because the compiler adds an s_cmp_eq 0 after the s_and (one more SALU per token,
 // and SALU issue is what bounds this kernel).  The order is the compiler's own hazard-clean one.
 template <uint32_t STOPMASK = 0x1C0C0u>
-__device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
-    uint32_t t, tmp;
+__device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X, uint32_t &t) {
+    uint32_t tmp;   // t: the last token word walked (the round's carry when it crosses 64 bytes)
     asm volatile(
         "1:\n\t"
         "v_readlane_b32 %[t], %[vt], %[X]\n\t"
@@ -478,6 +478,21 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
         : [vt] "v"(vt), [M] "i"(STOPMASK)
         : "m0", "scc");
 }
+template <uint32_t STOPMASK = 0x1C0C0u>
+__device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
+    uint32_t t;
+    walk_asm<STOPMASK>(vt, vtin, X, t);
+}
+#ifdef PPG_R4_ALATCH
+// the round loop's latch limit: 0 after a special token (bit 7 of the walk state), else lim -- as
+// one opaque s_bitcmp1 + s_cselect, so the latch stays one s_cmp + s_cbranch (the compiler turned
+// "spec ? 0 : lim" into 64-bit lane-mask logic: 5 SALU)
+__device__ __forceinline__ uint32_t latch_limit(uint32_t x, uint32_t lim) {
+    uint32_t r;
+    asm("s_bitcmp1_b32 %1, 7\n\ts_cselect_b32 %0, 0, %2" : "=s"(r) : "s"(uni(x)), "s"(uni(lim)) : "scc");
+    return r;
+}
+#endif
 
 // (r03 tried a walk taking two tokens per step -- each candidate's following token gathered by one
 // ds_bpermute per span, the v_readlane -> s_add -> v_readlane chain paid once per two tokens:
@@ -491,8 +506,13 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
 // r03 v4: the token rounds as an inner loop with one latch, and the emit's token-start address as
 // one v_mad_i32_i24 -- together 694.5 -> 682.2 ms per 50 GB step (each alone: 695.1 / 701.0;
 // profiles/r03_ab_latch_sj.txt).
+#ifdef PPG_R4_W8
+#define PPG_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))   // hold the VGPRs to 64
+#else
+#define PPG_WAVES_ATTR
+#endif
 template <int RB, int LBT, bool IX, bool CEN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_ATTR void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
@@ -751,12 +771,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
 #else
         using SpecT = bool;
 #endif
-        struct Round { uint32_t vtin, off, adv; SpecT spec; };
+        // tl: the last token word walked -- the carry when the round's tokens cross 64 bytes (TLAST);
+        // xr: the walk's final state, bit 7 = stopped at a special token (ALATCH)
+        struct Round { uint32_t vtin, off, adv; SpecT spec; uint32_t tl, xr; };
         // the five stream words a lane decodes from at bit bp (st_enter made their segments resident)
         struct Words { uint32_t x0, x1, x2, x3, x4; };
         auto words = [&](uint32_t bp) -> Words {
+#ifdef PPG_R4_WIDX
+            // (bp >> 5) + (((bp & 31) + lane) >> 5) == (bp + lane) >> 5: the word index in VALU only
+            const uint32_t *sw = S.stream + __builtin_amdgcn_ubfe(bp + (uint32_t)lane, 5u, 7u);
+#else
             const uint32_t o = (bp & 31) + (uint32_t)lane;                      // 0..94
             const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
+#endif
             return Words{sw[0], sw[1], sw[2], sw[3], sw[4]};
         };
 #ifdef PPG_R4_HOT
@@ -767,13 +794,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
             constexpr bool HOT = false;
 #endif
             uint32_t s = 0, off = cn, t = 0, half = 0;
-            uint32_t vtin = 0;
+            uint32_t vtin = 0, tl = cw, xr = 0;   // no walk (cn >= 64): the carried word stays
+#ifdef PPG_R4_CARRY
+            // lane 0 unconditionally: with no carry (cn == 0) the walk's first token overwrites it
+            vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
+#else
             if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
+#endif
             SpecT spec = 0;
             if (off < (HOT ? 64u : min(64u, len - pos))) {
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring, read during the previous round's emit)
+#ifdef PPG_R4_WIDX
+                const uint32_t o = bp + (uint32_t)lane;   // v_alignbit reads only bits [4:0]
+#else
                 const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
+#endif
                 const uint32_t x0 = W.x0, x1 = W.x1, x2 = W.x2, x3 = W.x3, x4 = W.x4;
                 // speculative tokens at every bit offset of the 128-bit span (two per lane)
                 const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
@@ -799,11 +835,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
                 if (HOT || len - pos >= 64) {
                     X = off << 8;
                     asm volatile("s_setprio 2");
-                    walk_asm(vta, vtin, X);
+                    walk_asm(vta, vtin, X, tl);
                     if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
                         X -= 64;
                         half = 64;
-                        walk_asm(vtb, vtin, X);
+                        walk_asm(vtb, vtin, X, tl);
                     }
                     asm volatile("s_setprio 1");
                     off = (X >> 8) & 511u;
@@ -825,11 +861,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
                         } while ((X & STOP) == 0u);
                     }
                     off = ((X >> 8) & 511u) - cl;
+                    tl = t;
                 }
+                xr = X;
                 spec = (SpecT)(X & 128u);
                 s = half + (X & 127u);   // bit offset of the next token (of the special one: bit 7 dropped)
             }
-            return Round{vtin, off, s, spec};
+            return Round{vtin, off, s, spec, tl, xr};
         };
 
         st_enter(r, S.stream, bp >> 10, lane);
@@ -838,7 +876,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
         // one round (decode + walk, one output byte per lane); HOT: at least 322 output bytes are left
         // (a round's tokens cover at most 63 + 258), so neither the walk's stop nor the emitted bytes
         // need the chunk's end -- the rounds of the chunk's last 322 bytes run the general form
-        auto one_round = [&](auto hot) -> SpecT {
+#ifdef PPG_R4_ALATCH
+        using RoundRet = uint32_t;   // the walk's final state: bit 7 = a special token ended the round
+#else
+        using RoundRet = SpecT;
+#endif
+        auto one_round = [&](auto hot) -> RoundRet {
             constexpr bool HOT = decltype(hot)::value;
             PPG_STAMP(t0);
             const Round R = decode(hot, bp, cn, cw, pos, W);
@@ -891,6 +934,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
                 sa_rd += t2 - t1;
 #endif
                 if (fm) {
+#ifdef PPG_R4_LATE
+                  if constexpr (HOT && !IX) {
+                    // LATE: hot rounds start at pos >= 32768, so a far source is never in the window
+                    const uint32_t b = far_load_u8(ob, far ? (uint32_t)jj + (pos + oa) : 0u);
+                    val = far ? b : val;
+                  } else
+#endif
+                  {
                     // older than the ring: the flushed output (this wave's own earlier stores), as
                     // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
                     // juggling); references into the Point's window (first 32 KiB only) separately
@@ -913,6 +964,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
                         else db = dict[fd ? 32768u + (uint32_t)p : 0u];       // p >= -32768
                         val = fd ? db : val;
                     }
+                  }
                 }
 #ifdef PPG_STAMPS
                 const uint64_t t3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
@@ -944,9 +996,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
 #endif
             }
             cn = tot - rout;
+#if defined(PPG_R4_TLAST)
+            // the walk's last token is the one crossing the round's 64 bytes whenever cn > 0 (no
+            // lane read, no branch; unused when cn == 0)
+            cw = R.tl & ~(511u << 8);
+#elif defined(PPG_R4_CARRY)
+            // the carried word is read every round (no branch); unused when cn == 0 (see decode)
+            cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
+#else
             if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
                 cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
             }
+#endif
             pos += rout;
 #ifndef PPG_R4_LIM
             if (pos >= fl_next) {
@@ -958,13 +1019,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
             bp += R.adv;
             asm volatile("s_setprio 0");
             if constexpr (IX) {   // past the member, or runaway output (a false start)
-                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; return true; }
+                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; return (RoundRet)128u; }
             }
 #ifdef PPG_STAMPS
             sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
             st_w0 = 0;
 #endif
+#ifdef PPG_R4_ALATCH
+            return R.xr;
+#else
             return R.spec;
+#endif
         };
 #endif
         for (;;) {
@@ -980,17 +1045,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) void ppg_i
 #ifdef PPG_R4_HOT
           {
               const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
+#ifdef PPG_R4_LATE
+              if (pos >= 32768u && pos < limh) {
+#else
               if (pos < limh) {
+#endif
+#ifdef PPG_R4_ALATCH
+                  do {
+                      lim_r = latch_limit(one_round(std::true_type{}), limh);
+                  } while (pos < lim_r);
+                  spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
+#else
                   do {
                       spec_ = one_round(std::true_type{});
                       lim_r = spec_ ? 0u : limh;
                   } while (pos < lim_r);
+#endif
               }
               if (!spec_ && pos < lim) {
+#ifdef PPG_R4_ALATCH
+                  do {
+                      lim_r = latch_limit(one_round(std::false_type{}), lim);
+                  } while (pos < lim_r);
+                  spec_ = lim_r == 0u;
+#else
                   do {
                       spec_ = one_round(std::false_type{});
                       lim_r = spec_ ? 0u : lim;
                   } while (pos < lim_r);
+#endif
               }
           }
           if (false)
