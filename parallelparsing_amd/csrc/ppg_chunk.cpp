@@ -143,6 +143,7 @@ struct FindChunk {
     uint64_t bit0, bit1;                // compressed bits of the chunk: [from's start bit, slice end)
     uint64_t bit_end;                   // to's block start (8 to.Input - to.Bits), or bit1 for the last chunk
     int64_t out0;                       // the chunk's first output byte (launch coordinates)
+    int64_t len;                        // the chunk's output bytes
     const uint8_t *window;              // the Point's 32 KiB
 };
 
@@ -230,19 +231,30 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
     HIPCHK(ppg_launch_gather(s, F.ring.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * np)));
     // the chains: piece j of a chunk is followed when its last block end is piece j+1's start
     std::vector<std::vector<uint32_t>> chain(ch.size());
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> ends(ch.size());   // (bit, chunk-relative output)
+    // the side point of a chain end is the FIRST block end of its piece with the same output: a
+    // sync flush's empty stored block (pigz, Z_SYNC_FLUSH) ends at the same output as the block
+    // before it, and the split decode of the piece before a side point stops (pos == len, the
+    // end-of-block consumed) at that first end, not past the empty block (a side point there was
+    // a DATA_ERROR in ppg_split_merge).  An end that adds no output, or reaches the chunk's end,
+    // is walked through but gets no side point (keep = 0).
+    struct End { uint64_t bit, out; bool keep; };
+    std::vector<std::vector<End>> ends(ch.size());   // chunk-relative output
     for (size_t c = 0; c < ch.size(); c++) {
-        uint64_t outc = 0;
+        uint64_t outc = 0, last_kept = 0;
         for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) {
             const PpgInflateResult &r = res[q];
             const uint32_t nb = std::min(r.nblocks, jobs[q].blk_cap);
             if (r.status != 0 || nb == 0 || r.last || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN))) break;
-            const PpgBlockEnd &B = blk[jobs[q].blk_off + nb - 1];
-            const uint64_t E = B.end_bit;
-            if (E >= ch[c].bit_end || B.out_end != r.produced) break;
+            const PpgBlockEnd *bl = blk.data() + jobs[q].blk_off;
+            const uint64_t E = bl[nb - 1].end_bit;
+            if (E >= ch[c].bit_end || bl[nb - 1].out_end != r.produced) break;
+            uint32_t f = nb - 1;
+            while (f > 0 && bl[f - 1].out_end == bl[nb - 1].out_end) f--;
             outc += r.produced;
+            const bool keep = outc > last_kept && (int64_t)outc < ch[c].len;
+            if (keep) last_kept = outc;
             chain[c].push_back((uint32_t)q);
-            ends[c].push_back({E, outc});
+            ends[c].push_back(End{bl[f].end_bit, outc, keep});
             if (q + 1 >= pfirst[c + 1] || pc[q + 1].start != E) break;   // the next candidate was false
         }
     }
@@ -268,19 +280,24 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
     }
     const size_t base = sbit.size();
     size_t nnew = 0;
-    for (size_t c = 0; c < ch.size(); c++) nnew += chain[c].size();
+    for (size_t c = 0; c < ch.size(); c++)
+        for (const End &e : ends[c]) nnew += e.keep;
     swin.resize((base + nnew) * kWin);
     size_t t = base;
     for (size_t c = 0; c < ch.size(); c++) {
-        if (chain[c].empty()) continue;
-        HIPCHK(hipMemcpyAsync(swin.data() + t * kWin, F.W.p + (c * wmax + 1) * kWin, chain[c].size() * kWin,
-                              hipMemcpyDeviceToHost, s));
-        nsplit++;
-        for (const auto &e : ends[c]) {
-            sbit.push_back((int64_t)e.first);
-            sout.push_back(ch[c].out0 + (int64_t)e.second);
+        bool any = false;
+        for (size_t j = 0; j < ends[c].size(); j++) {
+            const End &e = ends[c][j];
+            if (!e.keep) continue;
+            // W[j + 1]: the history at the end of chain piece j (an empty block adds none)
+            HIPCHK(hipMemcpyAsync(swin.data() + t * kWin, F.W.p + (c * wmax + j + 1) * kWin, kWin,
+                                  hipMemcpyDeviceToHost, s));
+            sbit.push_back((int64_t)e.bit);
+            sout.push_back(ch[c].out0 + (int64_t)e.out);
+            t++;
+            any = true;
         }
-        t += chain[c].size();
+        nsplit += any;
     }
     HIPCHK(hipStreamSynchronize(s));
     return PPG_OK;
@@ -367,7 +384,7 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
                 // sorted by output with the others: flush the found ones in launch order
                 const PpgInflateJob &J = sh->h_jobs[i];
                 find.push_back(FindChunk{J.bit_start, J.bit_limit, J.expect_end != ~0ull ? J.expect_end : J.bit_limit,
-                                         sh->h_pout[i], go[i]->ix->win((size_t)go[i]->k)});
+                                         sh->h_pout[i], (int64_t)J.out_len, go[i]->ix->win((size_t)go[i]->k)});
             }
             if (!find.empty() && (i + 1 == go.size() || !go[i + 1]->ix->side_out.empty())) {
                 const size_t before = sbit.size();

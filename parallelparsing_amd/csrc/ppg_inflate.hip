@@ -110,9 +110,6 @@ struct Reader {
     uint32_t wi;            // next word to append to bb
     uint64_t bb;            // bit buffer, LSB = next bit
     uint32_t bn;            // valid bits in bb
-#ifdef PPG_R4_SGB
-    uint32_t sgb;           // (sg + 1) << 10: the first stream bit past the segment the decoder is in
-#endif
 };
 
 // global_load_lds_dword as inline asm: with the builtin the compiler waits for the DMA (vmcnt) before
@@ -142,9 +139,6 @@ __device__ __forceinline__ void st_enter(Reader &r, uint32_t *stream, uint32_t g
     }
     st_issue(r, stream, g + 2, lane);
     r.sg = g;
-#ifdef PPG_R4_SGB
-    r.sgb = (g + 1) << 10;
-#endif
     asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
 }
 
@@ -478,12 +472,6 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
         : [vt] "v"(vt), [M] "i"(STOPMASK)
         : "m0", "scc");
 }
-template <uint32_t STOPMASK = 0x1C0C0u>
-__device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X) {
-    uint32_t t;
-    walk_asm<STOPMASK>(vt, vtin, X, t);
-}
-#ifdef PPG_R4_ALATCH
 // the round loop's latch limit: 0 after a special token (bit 7 of the walk state), else lim -- as
 // one opaque s_bitcmp1 + s_cselect, so the latch stays one s_cmp + s_cbranch (the compiler turned
 // "spec ? 0 : lim" into 64-bit lane-mask logic: 5 SALU)
@@ -492,7 +480,6 @@ __device__ __forceinline__ uint32_t latch_limit(uint32_t x, uint32_t lim) {
     asm("s_bitcmp1_b32 %1, 7\n\ts_cselect_b32 %0, 0, %2" : "=s"(r) : "s"(uni(x)), "s"(uni(lim)) : "scc");
     return r;
 }
-#endif
 
 // (r03 tried a walk taking two tokens per step -- each candidate's following token gathered by one
 // ds_bpermute per span, the v_readlane -> s_add -> v_readlane chain paid once per two tokens:
@@ -506,13 +493,10 @@ __device__ __forceinline__ uint32_t latch_limit(uint32_t x, uint32_t lim) {
 // r03 v4: the token rounds as an inner loop with one latch, and the emit's token-start address as
 // one v_mad_i32_i24 -- together 694.5 -> 682.2 ms per 50 GB step (each alone: 695.1 / 701.0;
 // profiles/r03_ab_latch_sj.txt).
-#ifdef PPG_R4_W8
-#define PPG_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))   // hold the VGPRs to 64
-#else
-#define PPG_WAVES_ATTR
-#endif
+// amdgpu_waves_per_eu(8, 8): the VGPRs held to 64 (r04: the round loop's carry state took the
+// compiler to 65, 7 waves per SIMD)
 template <int RB, int LBT, bool IX, bool CEN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_ATTR void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
@@ -572,9 +556,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
     const uint64_t w0abs = (J.bit_start >> 5) & ~127ull;
     Reader r;
     r.sg = 0x7FFFFFF0u;   // nothing resident: the first seek loads
-#ifdef PPG_R4_SGB
-    r.sgb = 0;
-#endif
     r.base = comp + w0abs;
     r.nw = (uint32_t)min(nwords > w0abs ? nwords - w0abs : 1ull, 0xFFFFFFFFull);
     const uint32_t bit_limit = (uint32_t)min(J.bit_limit - w0abs * 32, 0xFFFFFFFFull);   // < 2^32 - 2^12: ppg_index_validate
@@ -634,9 +615,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
 
     while (pos < len && !last) {
         r.sg = uni(r.sg);
-#ifdef PPG_R4_SGB
-        r.sgb = uni(r.sgb);
-#endif
         r.wi = uni(r.wi);
         r.bb = uni64(r.bb);
         r.bn = uni(r.bn);
@@ -742,9 +720,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
         // through the outer loop), so the token rounds keep it in SGPRs with scalar branches
         r.sg = uni(r.sg);
-#ifdef PPG_R4_SGB
-        r.sgb = uni(r.sgb);
-#endif
         r.wi = uni(r.wi);
         r.bb = uni64(r.bb);
         r.bn = uni(r.bn);
@@ -764,52 +739,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
         uint32_t cn = 0, cw = 0;   // carried: bytes left of the last round's last match, its token word
 
         // decode of the round starting at output position pos, stream bit bp, carry (cn, cw):
-        // returns the token words placed at their output offsets, the output bytes the round's
-        // tokens cover (off), the bit advance (adv) and whether it stopped at a special token
-#ifdef PPG_R4_ISPEC
-        using SpecT = uint32_t;   // 128 for a special token: an integer the compiler keeps in one SGPR
-#else
-        using SpecT = bool;
-#endif
-        // tl: the last token word walked -- the carry when the round's tokens cross 64 bytes (TLAST);
-        // xr: the walk's final state, bit 7 = stopped at a special token (ALATCH)
-        struct Round { uint32_t vtin, off, adv; SpecT spec; uint32_t tl, xr; };
-        // the five stream words a lane decodes from at bit bp (st_enter made their segments resident)
+        // returns the token words placed at their output offsets (vtin), the output bytes the
+        // round's tokens cover (off), the bit advance (adv), the last token word walked (tl: the
+        // carry whenever the round's tokens cross 64 bytes) and the walk's final state (xr: bit 7 =
+        // it stopped at a special token)
+        struct Round { uint32_t vtin, off, adv, tl, xr; };
+        // the five stream words a lane decodes from at bit bp (st_enter made their segments
+        // resident): (bp >> 5) + (((bp & 31) + lane) >> 5) == (bp + lane) >> 5, in VALU only
         struct Words { uint32_t x0, x1, x2, x3, x4; };
         auto words = [&](uint32_t bp) -> Words {
-#ifdef PPG_R4_WIDX
-            // (bp >> 5) + (((bp & 31) + lane) >> 5) == (bp + lane) >> 5: the word index in VALU only
             const uint32_t *sw = S.stream + __builtin_amdgcn_ubfe(bp + (uint32_t)lane, 5u, 7u);
-#else
-            const uint32_t o = (bp & 31) + (uint32_t)lane;                      // 0..94
-            const uint32_t *sw = S.stream + (((bp >> 5) + (o >> 5)) & 127);
-#endif
             return Words{sw[0], sw[1], sw[2], sw[3], sw[4]};
         };
-#ifdef PPG_R4_HOT
+        // HOT: at least 322 output bytes are left (a round's tokens cover at most 63 + 258), so
+        // neither the walk's stop nor the emitted bytes need the chunk's end, and pos >= 32768, so
+        // no far source lies in the Point's window
         auto decode = [&](auto hot, uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos, const Words &W) -> Round {
             constexpr bool HOT = decltype(hot)::value;
-#else
-        auto decode = [&](uint32_t bp, uint32_t cn, uint32_t cw, uint32_t pos, const Words &W) -> Round {
-            constexpr bool HOT = false;
-#endif
             uint32_t s = 0, off = cn, t = 0, half = 0;
-            uint32_t vtin = 0, tl = cw, xr = 0;   // no walk (cn >= 64): the carried word stays
-#ifdef PPG_R4_CARRY
+            uint32_t tl = cw, xr = 0;   // no walk (cn >= 64): the carried word stays
             // lane 0 unconditionally: with no carry (cn == 0) the walk's first token overwrites it
-            vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
-#else
-            if (cn) vtin = (uint32_t)llvm_writelane((int)cw, 0, (int)vtin);
-#endif
-            SpecT spec = 0;
+            uint32_t vtin = (uint32_t)llvm_writelane((int)cw, 0, 0);
             if (off < (HOT ? 64u : min(64u, len - pos))) {
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
-                // ring, read during the previous round's emit)
-#ifdef PPG_R4_WIDX
-                const uint32_t o = bp + (uint32_t)lane;   // v_alignbit reads only bits [4:0]
-#else
-                const uint32_t o = (bp & 31) + (uint32_t)lane;                  // 0..94
-#endif
+                // ring, read during the previous round's emit); v_alignbit reads only bits [4:0]
+                const uint32_t o = bp + (uint32_t)lane;
                 const uint32_t x0 = W.x0, x1 = W.x1, x2 = W.x2, x3 = W.x3, x4 = W.x4;
                 // speculative tokens at every bit offset of the 128-bit span (two per lane)
                 const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
@@ -864,34 +818,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
                     tl = t;
                 }
                 xr = X;
-                spec = (SpecT)(X & 128u);
                 s = half + (X & 127u);   // bit offset of the next token (of the special one: bit 7 dropped)
             }
-            return Round{vtin, off, s, spec, tl, xr};
+            return Round{vtin, off, s, tl, xr};
         };
 
         st_enter(r, S.stream, bp >> 10, lane);
         Words W = words(bp);
-#ifdef PPG_R4_HOT
-        // one round (decode + walk, one output byte per lane); HOT: at least 322 output bytes are left
-        // (a round's tokens cover at most 63 + 258), so neither the walk's stop nor the emitted bytes
-        // need the chunk's end -- the rounds of the chunk's last 322 bytes run the general form
-#ifdef PPG_R4_ALATCH
-        using RoundRet = uint32_t;   // the walk's final state: bit 7 = a special token ended the round
-#else
-        using RoundRet = SpecT;
-#endif
-        auto one_round = [&](auto hot) -> RoundRet {
+        // One round: decode + walk, then one output byte per lane.  Returns the walk's final state
+        // (bit 7: a special token ended the round).
+        auto one_round = [&](auto hot) -> uint32_t {
             constexpr bool HOT = decltype(hot)::value;
             PPG_STAMP(t0);
             const Round R = decode(hot, bp, cn, cw, pos, W);
             // the next round's stream words, read now: their LDS latency overlaps this round's
             // emit instead of opening the next round's chain of dependent LDS reads (r03)
-#ifdef PPG_R4_SGB
-            if (bp + R.adv >= r.sgb) st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
-#else
             st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
-#endif
             W = words(bp + R.adv);
 #ifdef PPG_STAMPS
             const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
@@ -903,7 +845,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
 #ifdef PPG_STATS
             st_rounds++;
             st_tokens += (uint32_t)__popcll(__ballot(R.vtin != 0));
-            if (R.spec) st_spec++;
+            if (R.xr & 128u) st_spec++;
             if (R.off < 64) st_short++;
 #endif
             const uint32_t tot = HOT ? R.off : min(R.off, len - pos);   // output bytes of the round's tokens
@@ -934,16 +876,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
                 sa_rd += t2 - t1;
 #endif
                 if (fm) {
-#ifdef PPG_R4_LATE
                   if constexpr (HOT && !IX) {
-                    // LATE: hot rounds start at pos >= 32768, so a far source is never in the window
+                    // pos >= 32768: the source is the flushed output, one byte load at ob + oa + p
                     const uint32_t b = far_load_u8(ob, far ? (uint32_t)jj + (pos + oa) : 0u);
                     val = far ? b : val;
-                  } else
-#endif
-                  {
+                  } else {
                     // older than the ring: the flushed output (this wave's own earlier stores), as
-                    // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
+                    // one saddr load for the whole wave (non-far lanes read out[0]: no exec
                     // juggling); references into the Point's window (first 32 KiB only) separately
                     const int32_t p = (int32_t)pos + jj;
                     const bool fo = far && p >= 0;
@@ -996,222 +935,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
 #endif
             }
             cn = tot - rout;
-#if defined(PPG_R4_TLAST)
-            // the walk's last token is the one crossing the round's 64 bytes whenever cn > 0 (no
-            // lane read, no branch; unused when cn == 0)
+            // the walk's last token is the one crossing the round's 64 bytes whenever cn > 0: the
+            // carry, as a match (bytes field 0) -- no lane read, no branch; unused when cn == 0
             cw = R.tl & ~(511u << 8);
-#elif defined(PPG_R4_CARRY)
-            // the carried word is read every round (no branch); unused when cn == 0 (see decode)
-            cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
-#else
-            if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
-                cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
-            }
-#endif
             pos += rout;
-#ifndef PPG_R4_LIM
-            if (pos >= fl_next) {
-                flush(fl_done, fl_next);
-                fl_done = fl_next;
-                fl_next += UNIT;
-            }
-#endif
             bp += R.adv;
             asm volatile("s_setprio 0");
             if constexpr (IX) {   // past the member, or runaway output (a false start)
-                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; return (RoundRet)128u; }
+                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; return 128u; }
             }
 #ifdef PPG_STAMPS
             sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
             st_w0 = 0;
 #endif
-#ifdef PPG_R4_ALATCH
             return R.xr;
-#else
-            return R.spec;
-#endif
         };
-#endif
         for (;;) {
-          // the token rounds as an inner loop with ONE latch (not special, output left): the two
-          // exits of the plain form made the compiler merge them through an exit-selector register
-          SpecT spec_ = 0;
-#ifdef PPG_R4_LIM
-          // one compare per round leaves the rounds for all three reasons: a flush boundary, the end
-          // of the output, a special token (whose limit is 0)
-          const uint32_t lim = min(len, fl_next);
-          uint32_t lim_r;
-#endif
-#ifdef PPG_R4_HOT
-          {
-              const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
-#ifdef PPG_R4_LATE
-              if (pos >= 32768u && pos < limh) {
-#else
-              if (pos < limh) {
-#endif
-#ifdef PPG_R4_ALATCH
-                  do {
-                      lim_r = latch_limit(one_round(std::true_type{}), limh);
-                  } while (pos < lim_r);
-                  spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
-#else
-                  do {
-                      spec_ = one_round(std::true_type{});
-                      lim_r = spec_ ? 0u : limh;
-                  } while (pos < lim_r);
-#endif
-              }
-              if (!spec_ && pos < lim) {
-#ifdef PPG_R4_ALATCH
-                  do {
-                      lim_r = latch_limit(one_round(std::false_type{}), lim);
-                  } while (pos < lim_r);
-                  spec_ = lim_r == 0u;
-#else
-                  do {
-                      spec_ = one_round(std::false_type{});
-                      lim_r = spec_ ? 0u : lim;
-                  } while (pos < lim_r);
-#endif
-              }
-          }
-          if (false)
-#endif
-          do {
-            // ---- one round: decode + walk, then one output byte per lane ----
-            PPG_STAMP(t0);
-#ifdef PPG_R4_HOT
-            const Round R = decode(std::false_type{}, bp, cn, cw, pos, W);
-#else
-            const Round R = decode(bp, cn, cw, pos, W);
-#endif
-            // the next round's stream words, read now: their LDS latency overlaps this round's
-            // emit instead of opening the next round's chain of dependent LDS reads (r03)
-#ifdef PPG_R4_SGB
-            if (bp + R.adv >= r.sgb) st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
-#else
-            st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
-#endif
-            W = words(bp + R.adv);
-#ifdef PPG_STAMPS
-            const uint64_t t1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
-            if (st_w0 < t0) st_w0 = t1;   // no walk this round
-            sa_dec += st_w0 - t0;
-            sa_walk += t1 - st_w0;
-            sa_rounds++;
-#endif
-#ifdef PPG_STATS
-            st_rounds++;
-            st_tokens += (uint32_t)__popcll(__ballot(R.vtin != 0));
-            if (R.spec) st_spec++;
-            if (R.off < 64) st_short++;
-#endif
-            const uint32_t tot = min(R.off, len - pos);   // output bytes of the round's tokens
-            const uint32_t rout = min(tot, 64u);          // ... emitted this round
-            const uint64_t mo = __ballot(R.vtin != 0);    // token start offsets (never 0 words)
-            // All 64 lanes write: lanes past rout leave garbage in the slots of positions
-            // [pos + rout, pos + 64), which later rounds overwrite before use; the slots' previous
-            // bytes (positions >= pos + rout - RING) are therefore never read from the ring —
-            // references reach back at most RING - 64 bytes (REACH), older bytes come from HBM.
+            // The rounds up to the next flush boundary (or the output's end) as inner loops with ONE
+            // latch each: pos < lim_r, where lim_r = 0 once a special token ended a round
+            // (latch_limit), so one compare leaves the rounds for all three reasons.  The HOT loop
+            // runs the rounds at least 32 KiB into the chunk and 322 bytes before its end; the
+            // general form the others.  (r04: 679.2 -> 641.8 ms per 50 GB step in one same-box A/B,
+            // profiles/r04_ab_round_control.json.)
+            const uint32_t lim = min(len, fl_next);
+            uint32_t lim_r = 1;
             {
-                // 4 * (63 - clz) in one v_mad_i32_i24 (the compiler's form: shift + xor)
-                uint32_t sj4;
-                asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
-                const uint32_t inf = bperm(sj4, R.vtin);
-                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);   // source, relative to the round
-                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                uint32_t val;   // (IX: a literal is the symbol 0x8000 | byte; written apart, the DecompressAll
-                                // instance's code is unchanged -- the folded "| 0" moved its schedule)
-                if constexpr (IX) val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
-                else val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-                const bool far = jj < -(int32_t)(RING - 64);          // far (literals: jj >= -512)
-                const uint64_t fm = __ballot(far);
-#ifdef PPG_STATS
-                if (fm) st_far++;
-#endif
-#ifdef PPG_STAMPS
-                const uint64_t t2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
-                sa_rd += t2 - t1;
-#endif
-                if (fm) {
-                    // older than the ring: the flushed output (this wave's own earlier stores), as
-                    // one saddr dword load for the whole wave (non-far lanes read out[0]: no exec
-                    // juggling); references into the Point's window (first 32 KiB only) separately
-                    const int32_t p = (int32_t)pos + jj;
-                    const bool fo = far && p >= 0;
-                    if constexpr (IX) {
-                        const uint32_t q = 2u * ((uint32_t)p & IX_RING_MASK);
-                        const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
-                        val = fo ? __builtin_amdgcn_ubfe(w, q << 3, 16u) : val;
-                    } else {
-                        // one byte load at ob + oa + p (pos + oa is wave-uniform)
-                        const uint32_t b = far_load_u8(ob, fo ? (uint32_t)jj + (pos + oa) : 0u);
-                        val = fo ? b : val;
-                    }
-                    const bool fd = far && p < 0;
-                    const uint64_t dm = fm & __ballot(p < 0);   // (a ballot of fd itself went through two VALU)
-                    if (dm) {   // rare: the chunk's first 32 KiB
-                        uint32_t db;
-                        if constexpr (IX) db = 32768u + (uint32_t)p;          // the history symbol itself
-                        else db = dict[fd ? 32768u + (uint32_t)p : 0u];       // p >= -32768
-                        val = fd ? db : val;
-                    }
+                const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
+                if (pos >= 32768u && pos < limh) {
+                    do {
+                        lim_r = latch_limit(one_round(std::true_type{}), limh);
+                    } while (pos < lim_r);
                 }
-#ifdef PPG_STAMPS
-                const uint64_t t3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
-                sa_far += t3 - t2;
-                sa_farr += fm ? 1 : 0;
-#endif
-                const bool dep = jj >= 0;                             // produced in this round
-                if (__ballot(dep)) {
-                    // chains inside the round (short distances): pointer doubling to a resolved byte
-                    int32_t ptr = dep ? jj : lane;
-#ifdef PPG_STATS
-                    st_dep++;
-#endif
-                    for (;;) {
-#ifdef PPG_STATS
-                        st_dbl++;
-#endif
-                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
-                        if (!__ballot(p2 != ptr)) break;
-                        ptr = p2;
-                    }
-                    val = bperm((uint32_t)ptr << 2, val);
+                if (lim_r && pos < lim) {
+                    do {
+                        lim_r = latch_limit(one_round(std::false_type{}), lim);
+                    } while (pos < lim_r);
                 }
-                S.ring[(rb0 + pos + lane) & RM] = (RingT)val;
-#ifdef PPG_STAMPS
-                const uint64_t t4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(val);
-                sa_dep += t4 - t3;
-                st_w0 = t4;   // reused below: start of the round's tail
-#endif
             }
-            cn = tot - rout;
-            if (cn) {   // the last token (a match) runs past this round: carry it, as a match (bytes field 0)
-                cw = rdlane(R.vtin, 63u - (uint32_t)__builtin_clzll(mo)) & ~(511u << 8);
-            }
-            pos += rout;
-#ifndef PPG_R4_LIM
-            if (pos >= fl_next) {
-                flush(fl_done, fl_next);
-                fl_done = fl_next;
-                fl_next += UNIT;
-            }
-#endif
-            bp += R.adv;
-            asm volatile("s_setprio 0");
-            if constexpr (IX) {   // past the member, or runaway output (a false start)
-                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; break; }
-            }
-#ifdef PPG_STAMPS
-            sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
-            st_w0 = 0;
-#endif
-            spec_ = R.spec;
-#ifdef PPG_R4_LIM
-            lim_r = spec_ ? 0u : lim;
-          } while (pos < lim_r);
+            const bool spec_ = lim_r == 0u;   // lim, limh > pos >= 0 otherwise
             if constexpr (IX) {
                 if (status != ST_OK) break;
             }
@@ -1224,11 +985,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80))) PPG_WAVES_
                 if (pos < len) continue;   // a flush boundary: more rounds
                 break;
             }
-#else
-          } while (!spec_ && pos < len);
-            if (!spec_) break;
-#endif
-
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
             asm volatile("s_setprio 2");
             rd_seek(r, S.stream, bp, lane);
