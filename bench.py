@@ -449,7 +449,7 @@ def create_index_run(tf, args, dev):
                               "projected_seconds_full_member": text / 1e9 / cpu_gbs}}
 
 
-def paired_run(args, dev, world=1, rank=0, xdev=None):
+def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
     """BASELINE configs[4]-shaped paired-end run: two tiled members (R1 / R2 of a read pair: equal
     spot numbers, different SRR ids and bases), chunk = 50,000, both decoded and resident, every
     record's spot key extracted on the GPU, Q1 duplicates dropped and the pair invariant checked
@@ -813,7 +813,7 @@ def main():
     from parallelparsing_amd.dist import partition_chunks, gather_counts
 
     if args.paired:
-        line = paired_run(args, dev, world, rank, xdev)
+        line = paired_run(args, dev, world, rank, xdev, backend)
         line["communicator"] = rccl_info(world, backend)
         if rank == 0:
             print(json.dumps(line), flush=True)

@@ -472,6 +472,38 @@ __device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &
         : [vt] "v"(vt), [M] "i"(STOPMASK)
         : "m0", "scc");
 }
+#ifdef PPG_WALK2
+// both spans' walks in one asm block: span b (candidates 64..127, X rebased by -64, half = 64) only
+// when span a ended at s >= 64 with output left and no special token (s_and's SCC decides)
+__device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vtin, uint32_t &X, uint32_t &t,
+                                          uint32_t &half) {
+    uint32_t tmp;
+    asm volatile(
+        "1:\n\t"
+        "v_readlane_b32 %[t], %[va], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc0 1b\n\t"
+        "s_mov_b32 %[h], 0\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c080\n\t"
+        "s_cbranch_scc1 3f\n\t"
+        "s_sub_u32 %[X], %[X], 64\n\t"
+        "s_mov_b32 %[h], 64\n"
+        "2:\n\t"
+        "v_readlane_b32 %[t], %[vb], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc0 2b\n"
+        "3:"
+        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp), [h] "=&s"(half)
+        : [va] "v"(va), [vb] "v"(vb)
+        : "m0", "scc");
+}
+#endif
 // the round loop's latch limit: 0 after a special token (bit 7 of the walk state), else lim -- as
 // one opaque s_bitcmp1 + s_cselect, so the latch stays one s_cmp + s_cbranch (the compiler turned
 // "spec ? 0 : lim" into 64-bit lane-mask logic: 5 SALU)
@@ -759,7 +791,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t tl = cw, xr = 0;   // no walk (cn >= 64): the carried word stays
             // lane 0 unconditionally: with no carry (cn == 0) the walk's first token overwrites it
+#ifdef PPG_CW0
+            uint32_t vtin = lane == 0 ? cw : 0u;
+#else
             uint32_t vtin = (uint32_t)llvm_writelane((int)cw, 0, 0);
+#endif
             if (off < (HOT ? 64u : min(64u, len - pos))) {
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring, read during the previous round's emit); v_alignbit reads only bits [4:0]
@@ -789,12 +825,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if (HOT || len - pos >= 64) {
                     X = off << 8;
                     asm volatile("s_setprio 2");
+#ifdef PPG_WALK2
+                    walk2_asm(vta, vtb, vtin, X, tl, half);
+#else
                     walk_asm(vta, vtin, X, tl);
                     if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
                         X -= 64;
                         half = 64;
                         walk_asm(vtb, vtin, X, tl);
                     }
+#endif
                     asm volatile("s_setprio 1");
                     off = (X >> 8) & 511u;
                 } else {
@@ -957,22 +997,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             // runs the rounds at least 32 KiB into the chunk and 322 bytes before its end; the
             // general form the others.  (r04: 679.2 -> 641.8 ms per 50 GB step in one same-box A/B,
             // profiles/r04_ab_round_control.json.)
+            bool spec_ = false;
             const uint32_t lim = min(len, fl_next);
-            uint32_t lim_r = 1;
+            uint32_t lim_r;
             {
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
                 if (pos >= 32768u && pos < limh) {
                     do {
                         lim_r = latch_limit(one_round(std::true_type{}), limh);
                     } while (pos < lim_r);
+                    spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
                 }
-                if (lim_r && pos < lim) {
+                if (!spec_ && pos < lim) {
                     do {
                         lim_r = latch_limit(one_round(std::false_type{}), lim);
                     } while (pos < lim_r);
+                    spec_ = lim_r == 0u;
                 }
             }
-            const bool spec_ = lim_r == 0u;   // lim, limh > pos >= 0 otherwise
             if constexpr (IX) {
                 if (status != ST_OK) break;
             }
