@@ -453,31 +453,16 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tok) : "v"(lm), "v"(t2), "v"(e));
     return tok;
 }
-// The walk loop of the decoder (see Round): per token v_readlane (candidate X[5:0]),
-// v_writelane (at output offset (X >> 8)[5:0]), one s_add, and s_and's SCC as the loop test —
-// written out because the compiler adds an s_cmp_eq 0 after the s_and (one more SALU per token,
-// and SALU issue is what bounds this kernel).  The order is the compiler's own hazard-clean one.
-template <uint32_t STOPMASK = 0x1C0C0u>
-__device__ __forceinline__ void walk_asm(uint32_t vt, uint32_t &vtin, uint32_t &X, uint32_t &t) {
-    uint32_t tmp;   // t: the last token word walked (the round's carry when it crosses 64 bytes)
-    asm volatile(
-        "1:\n\t"
-        "v_readlane_b32 %[t], %[vt], %[X]\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], %[M]\n\t"
-        "v_writelane_b32 %[vtin], %[t], m0\n\t"
-        "s_cbranch_scc0 1b"
-        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp)
-        : [vt] "v"(vt), [M] "i"(STOPMASK)
-        : "m0", "scc");
-}
-#ifdef PPG_WALK2
-// both spans' walks in one asm block: span b (candidates 64..127, X rebased by -64, half = 64) only
-// when span a ended at s >= 64 with output left and no special token (s_and's SCC decides)
+// The walk loop of the decoder (see Round) over both 64-candidate spans in one asm block: per
+// token v_readlane (candidate X[5:0]), v_writelane (at output offset (X >> 8)[5:0]), one s_add,
+// and s_and's SCC as the loop test; span b (candidates 64..127, X rebased by -64, half = 64) only
+// when span a ended at s >= 64 with output left and no special token (s_and's SCC again).  Written
+// out because the compiler adds an s_cmp_eq 0 after each s_and (one more SALU per token, and SALU
+// issue is what bounds this kernel); one block for both spans (r04: 642.3 -> 638.8 ms per 50 GB
+// step, same box, profiles/r04v2_ab_walk2_cw0_prio.json).  t: the last token word walked.
 __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vtin, uint32_t &X, uint32_t &t,
                                           uint32_t &half) {
-    uint32_t tmp;
+    uint32_t tmp;   // (the order is the compiler's own hazard-clean one for these instructions)
     asm volatile(
         "1:\n\t"
         "v_readlane_b32 %[t], %[va], %[X]\n\t"
@@ -503,7 +488,6 @@ __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vt
         : [va] "v"(va), [vb] "v"(vb)
         : "m0", "scc");
 }
-#endif
 // the round loop's latch limit: 0 after a special token (bit 7 of the walk state), else lim -- as
 // one opaque s_bitcmp1 + s_cselect, so the latch stays one s_cmp + s_cbranch (the compiler turned
 // "spec ? 0 : lim" into 64-bit lane-mask logic: 5 SALU)
@@ -791,11 +775,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             uint32_t s = 0, off = cn, t = 0, half = 0;
             uint32_t tl = cw, xr = 0;   // no walk (cn >= 64): the carried word stays
             // lane 0 unconditionally: with no carry (cn == 0) the walk's first token overwrites it
-#ifdef PPG_CW0
-            uint32_t vtin = lane == 0 ? cw : 0u;
-#else
             uint32_t vtin = (uint32_t)llvm_writelane((int)cw, 0, 0);
-#endif
             if (off < (HOT ? 64u : min(64u, len - pos))) {
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring, read during the previous round's emit); v_alignbit reads only bits [4:0]
@@ -825,17 +805,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if (HOT || len - pos >= 64) {
                     X = off << 8;
                     asm volatile("s_setprio 2");
-#ifdef PPG_WALK2
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-#else
-                    walk_asm(vta, vtin, X, tl);
-                    if ((X & (STOP & ~0x40u)) == 0u) {   // s in [64, 128): the second 64 offsets
-                        X -= 64;
-                        half = 64;
-                        walk_asm(vtb, vtin, X, tl);
-                    }
-#endif
+#ifndef PPG_PRIO2
                     asm volatile("s_setprio 1");
+#endif
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
