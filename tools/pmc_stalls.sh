@@ -11,7 +11,7 @@ timeout -s KILL 60 rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1 || true
 run() {
   g=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" -d gpurun_out/stall_$g -o pmc --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --repeats $R > gpurun_out/stall_$g.log 2>&1 || exit $?
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-enumerate --no-chunk-api --repeats $R > gpurun_out/stall_$g.log 2>&1 || exit $?
 }
 run A SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT
 run B SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU
