@@ -963,6 +963,65 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
 #endif
             return R.xr;
         };
+        // The HOT rounds software-pipelined (DecompressAll): a round's far load is issued at its
+        // emit and consumed at the next round's, after that round's decode and walk (which do not
+        // read the ring); the pending round is finished (far bytes merged, in-round chains resolved,
+        // ring written) before the next emit reads the ring, and at the loop's exit.  The far load
+        // (~1,000 cycles of a ~2,950-cycle round, PPG_STAMPS) now hides behind the next decode +
+        // walk: 640.8 -> 575.8 ms per 50 GB step in one same-box A/B
+        // (profiles/r04j_ab_pipelined_far.json).  (r02 tried the same on a kernel bound by SALU
+        // issue: no gain.)
+        auto hot_pipe = [&](uint32_t limh) -> uint32_t {
+            uint32_t p_val = 0, p_b = 0, p_pos = 0, lim_r;
+            int32_t p_jj = 0;
+            uint64_t p_fm = 0;
+            bool pend = false;
+            auto finish = [&]() {
+                uint32_t val = p_val;
+                if (p_fm) val = p_jj < -(int32_t)(RING - 64) ? p_b : val;
+                const bool dep = p_jj >= 0;
+                if (__ballot(dep)) {
+                    int32_t ptr = dep ? p_jj : lane;
+                    for (;;) {
+                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
+                        if (!__ballot(p2 != ptr)) break;
+                        ptr = p2;
+                    }
+                    val = bperm((uint32_t)ptr << 2, val);
+                }
+                S.ring[(rb0 + p_pos + lane) & RM] = (RingT)val;
+            };
+            do {
+                const Round R = decode(std::true_type{}, bp, cn, cw, pos, W);
+                st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
+                W = words(bp + R.adv);
+                if (pend) finish();
+                const uint32_t rout = min(R.off, 64u);
+                const uint64_t mo = __ballot(R.vtin != 0);
+                uint32_t sj4;
+                asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
+                const uint32_t inf = bperm(sj4, R.vtin);
+                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);
+                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
+                p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                const bool far = jj < -(int32_t)(RING - 64);
+                p_fm = __ballot(far);
+                // pos >= 32768: every far source is the flushed output; a compiler-tracked load (its
+                // s_waitcnt lands at the first use, in finish)
+                if (p_fm) p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
+                p_jj = jj;
+                p_pos = pos;
+                pend = true;
+                cn = R.off - rout;
+                cw = R.tl & ~(511u << 8);
+                pos += rout;
+                bp += R.adv;
+                asm volatile("s_setprio 0");
+                lim_r = latch_limit(R.xr, limh);
+            } while (pos < lim_r);
+            finish();
+            return lim_r;
+        };
         for (;;) {
             // The rounds up to the next flush boundary (or the output's end) as inner loops with ONE
             // latch each: pos < lim_r, where lim_r = 0 once a special token ended a round
@@ -976,9 +1035,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             {
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
                 if (pos >= 32768u && pos < limh) {
+                  if constexpr (!IX) {
+                    lim_r = hot_pipe(limh);
+                  } else {
                     do {
                         lim_r = latch_limit(one_round(std::true_type{}), limh);
                     } while (pos < lim_r);
+                  }
                     spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
                 }
                 if (!spec_ && pos < lim) {
