@@ -463,6 +463,47 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vtin, uint32_t &X, uint32_t &t,
                                           uint32_t &half) {
     uint32_t tmp;   // (the order is the compiler's own hazard-clean one for these instructions)
+#ifdef PPG_WUNR
+    // each span's loop unrolled by two: one taken branch per two tokens
+    asm volatile(
+        "1:\n\t"
+        "v_readlane_b32 %[t], %[va], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc1 4f\n\t"
+        "v_readlane_b32 %[t], %[va], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc0 1b\n"
+        "4:\n\t"
+        "s_mov_b32 %[h], 0\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c080\n\t"
+        "s_cbranch_scc1 3f\n\t"
+        "s_sub_u32 %[X], %[X], 64\n\t"
+        "s_mov_b32 %[h], 64\n"
+        "2:\n\t"
+        "v_readlane_b32 %[t], %[vb], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc1 3f\n\t"
+        "v_readlane_b32 %[t], %[vb], %[X]\n\t"
+        "s_lshr_b32 m0, %[X], 8\n\t"
+        "s_add_u32 %[X], %[t], %[X]\n\t"
+        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
+        "v_writelane_b32 %[vtin], %[t], m0\n\t"
+        "s_cbranch_scc0 2b\n"
+        "3:"
+        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp), [h] "=&s"(half)
+        : [va] "v"(va), [vb] "v"(vb)
+        : "m0", "scc");
+    return;
+#endif
     asm volatile(
         "1:\n\t"
         "v_readlane_b32 %[t], %[va], %[X]\n\t"
