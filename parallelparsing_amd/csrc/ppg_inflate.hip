@@ -847,9 +847,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                     X = off << 8;
                     asm volatile("s_setprio 2");
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-#ifndef PPG_PRIO2
                     asm volatile("s_setprio 1");
-#endif
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -930,11 +928,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 sa_rd += t2 - t1;
 #endif
                 if (fm) {
-                  if constexpr (HOT && !IX) {
-                    // pos >= 32768: the source is the flushed output, one byte load at ob + oa + p
-                    const uint32_t b = far_load_u8(ob, far ? (uint32_t)jj + (pos + oa) : 0u);
-                    val = far ? b : val;
-                  } else {
+                  {
                     // older than the ring: the flushed output (this wave's own earlier stores), as
                     // one saddr load for the whole wave (non-far lanes read out[0]: no exec
                     // juggling); references into the Point's window (first 32 KiB only) separately
@@ -1034,11 +1028,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             };
             do {
                 const Round R = decode(std::true_type{}, bp, cn, cw, pos, W);
-#ifndef PPG_PIPE3
-                st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
-                W = words(bp + R.adv);
-#endif
-#ifdef PPG_PIPE_BP
                 // the token lookup does not read the ring: issued before the pending round's finish
                 const uint32_t rout = min(R.off, 64u);
                 const uint64_t mo = __ballot(R.vtin != 0);
@@ -1046,18 +1035,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
                 const uint32_t inf = bperm(sj4, R.vtin);
                 if (pend) finish();
-#ifdef PPG_PIPE3
+                // the next round's stream words after the finish: the finish's s_waitcnt vmcnt(0)
+                // (the compiler's, for the far load) would otherwise also wait for a stream DMA
+                // issued here -- an HBM miss every ~9 rounds (574.6 -> 569.2 ms with the lookup
+                // above, profiles/r04l_ab_pipeline_variants.json)
                 st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
                 W = words(bp + R.adv);
-#endif
-#else
-                if (pend) finish();
-                const uint32_t rout = min(R.off, 64u);
-                const uint64_t mo = __ballot(R.vtin != 0);
-                uint32_t sj4;
-                asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
-                const uint32_t inf = bperm(sj4, R.vtin);
-#endif
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
@@ -1079,110 +1062,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             finish();
             return lim_r;
         };
-#ifdef PPG_PIPE2
-        // deeper: the next round's stream words are waited for and its litlen lookups issued
-        // between this round's finish and its emit (their LDS latency behind the emit)
-        struct Ph1 { uint32_t loa, hia, lob, hib, ea, eb; };
-        auto ph1 = [&](uint32_t bp, const Words &W) -> Ph1 {
-            const uint32_t o = bp + (uint32_t)lane;
-            Ph1 P;
-            P.loa = __builtin_amdgcn_alignbit(W.x1, W.x0, o);
-            P.hia = __builtin_amdgcn_alignbit(W.x2, W.x1, o);
-            P.lob = __builtin_amdgcn_alignbit(W.x3, W.x2, o);
-            P.hib = __builtin_amdgcn_alignbit(W.x4, W.x3, o);
-            P.ea = S.lit[P.loa & ((1u << LBT) - 1)];
-            P.eb = S.lit[P.lob & ((1u << LBT) - 1)];
-            return P;
-        };
-        auto ph2 = [&](const Ph1 &P, uint32_t lo, uint32_t hi, uint32_t e) -> uint32_t {
-            const uint32_t e2 = e >> 8;
-            const uint32_t y = __builtin_amdgcn_alignbit(hi, lo, e2);
-            uint32_t tke;
-            asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(tke) : "v"(__builtin_amdgcn_ubfe(lo, e, e2 - e)), "v"(e2));
-            const uint32_t d = S.dst[y & ((1u << DB) - 1)];
-            const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(y, d, d >> 10);
-            const uint32_t tlen = tke + ((d >> 5) & 31) + (dm1 << 17);
-            const uint32_t lm = (uint32_t)((int32_t)(e << 25) >> 31);
-            const uint32_t sd = (uint32_t)((int32_t)d >> 31);
-            uint32_t t2, tok;
-            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(t2) : "v"(sd), "v"(PPG_SPECIAL_TOKEN), "v"(tlen));
-            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tok) : "v"(lm), "v"(t2), "v"(e));
-            return tok;
-        };
-        auto hot_pipe2 = [&](uint32_t limh) -> uint32_t {
-            uint32_t p_val = 0, p_b = 0, p_pos = 0, lim_r;
-            int32_t p_jj = 0;
-            uint64_t p_fm = 0;
-            bool pend = false;
-            auto finish = [&]() {
-                uint32_t val = p_val;
-                if (p_fm) val = p_jj < -(int32_t)(RING - 64) ? p_b : val;
-                const bool dep = p_jj >= 0;
-                if (__ballot(dep)) {
-                    int32_t ptr = dep ? p_jj : lane;
-                    for (;;) {
-                        const int32_t p2 = (int32_t)bperm((uint32_t)ptr << 2, (uint32_t)ptr);
-                        if (!__ballot(p2 != ptr)) break;
-                        ptr = p2;
-                    }
-                    val = bperm((uint32_t)ptr << 2, val);
-                }
-                S.ring[(rb0 + p_pos + lane) & RM] = (RingT)val;
-            };
-            Ph1 P = ph1(bp, W);
-            do {
-                // round k: the rest of the decode, the walk
-                uint32_t vtin = (uint32_t)llvm_writelane((int)cw, 0, 0);
-                uint32_t off = cn, adv = 0, tl = cw, xr = 0;
-                {
-                    const uint32_t vta = ph2(P, P.loa, P.hia, P.ea), vtb = ph2(P, P.lob, P.hib, P.eb);
-                    if (off < 64u) {
-                        uint32_t X = off << 8, half;
-                        asm volatile("s_setprio 2");
-                        walk2_asm(vta, vtb, vtin, X, tl, half);
-                        asm volatile("s_setprio 1");
-                        off = (X >> 8) & 511u;
-                        xr = X;
-                        adv = half + (X & 127u);
-                    }
-                }
-#ifndef PPG_PIPE3
-                st_enter(r, S.stream, (bp + adv) >> 10, lane);
-                W = words(bp + adv);
-#endif
-                const uint32_t rout = min(off, 64u);
-                const uint64_t mo = __ballot(vtin != 0);
-                uint32_t sj4;
-                asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
-                const uint32_t inf = bperm(sj4, vtin);
-                if (pend) finish();
-#ifdef PPG_PIPE3
-                // after the finish: its s_waitcnt vmcnt(0) (the compiler's, for the far load) would
-                // otherwise also wait for a stream DMA issued here -- an HBM miss every ~9 rounds
-                st_enter(r, S.stream, (bp + adv) >> 10, lane);
-                W = words(bp + adv);
-#endif
-                P = ph1(bp + adv, W);   // round k+1's words and litlen lookups
-                const int32_t jj = lane - 1 - (int32_t)(inf >> 17);
-                const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-                const bool far = jj < -(int32_t)(RING - 64);
-                p_fm = __ballot(far);
-                if (p_fm) p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
-                p_jj = jj;
-                p_pos = pos;
-                pend = true;
-                cn = off - rout;
-                cw = tl & ~(511u << 8);
-                pos += rout;
-                bp += adv;
-                asm volatile("s_setprio 0");
-                lim_r = latch_limit(xr, limh);
-            } while (pos < lim_r);
-            finish();
-            return lim_r;
-        };
-#endif
         for (;;) {
             // The rounds up to the next flush boundary (or the output's end) as inner loops with ONE
             // latch each: pos < lim_r, where lim_r = 0 once a special token ended a round
@@ -1197,11 +1076,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
                 if (pos >= 32768u && pos < limh) {
                   if constexpr (!IX) {
-#ifdef PPG_PIPE2
-                    lim_r = hot_pipe2(limh);
-#else
                     lim_r = hot_pipe(limh);
-#endif
                   } else {
                     do {
                         lim_r = latch_limit(one_round(std::true_type{}), limh);
