@@ -847,7 +847,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                     X = off << 8;
                     asm volatile("s_setprio 2");
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-                    asm volatile("s_setprio 1");
+                    #ifndef PPG_PRIO2
+                    asm volatile("s_setprio 1");   // (PPG_PRIO2: the emit stays at 2; A/B switch)
+#endif
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -1007,13 +1009,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         // (profiles/r04j_ab_pipelined_far.json).  (r02 tried the same on a kernel bound by SALU
         // issue: no gain.)
         auto hot_pipe = [&](uint32_t limh) -> uint32_t {
+#ifdef PPG_LEAN
+            // no "pending" test: the loop starts with a dummy pending round (no far, no chain
+            // sources) whose 64 garbage bytes land in the slots of positions [pos, pos + 64),
+            // which the first real round's finish overwrites before anything reads them
+            uint32_t p_val = 0, p_b = 0, p_pos = pos, lim_r;
+            int32_t p_jj = -1;
+            constexpr bool pend = true;
+#else
             uint32_t p_val = 0, p_b = 0, p_pos = 0, lim_r;
             int32_t p_jj = 0;
             uint64_t p_fm = 0;
             bool pend = false;
+#endif
             auto finish = [&]() {
                 uint32_t val = p_val;
+#ifdef PPG_LEAN
+                val = p_jj < -(int32_t)(RING - 64) ? p_b : val;   // (no far lane: p_b unused)
+#else
                 if (p_fm) val = p_jj < -(int32_t)(RING - 64) ? p_b : val;
+#endif
                 const bool dep = p_jj >= 0;
                 if (__ballot(dep)) {
                     int32_t ptr = dep ? p_jj : lane;
@@ -1045,13 +1060,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 const bool far = jj < -(int32_t)(RING - 64);
-                p_fm = __ballot(far);
                 // pos >= 32768: every far source is the flushed output; a compiler-tracked load (its
                 // s_waitcnt lands at the first use, in finish)
+#ifdef PPG_LEAN
+                p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];   // 97% of rounds have a far lane
+#else
+                p_fm = __ballot(far);
                 if (p_fm) p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
+                pend = true;
+#endif
                 p_jj = jj;
                 p_pos = pos;
-                pend = true;
                 cn = R.off - rout;
                 cw = R.tl & ~(511u << 8);
                 pos += rout;
