@@ -463,8 +463,8 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vtin, uint32_t &X, uint32_t &t,
                                           uint32_t &half) {
     uint32_t tmp;   // (the order is the compiler's own hazard-clean one for these instructions)
-#ifdef PPG_WUNR
-    // each span's loop unrolled by two: one taken branch per two tokens
+    // each span's loop unrolled by two: one taken branch per two tokens (r04, on the pipelined
+    // kernel: 559.5 -> 553.8 ms, profiles/r04o_ab_lean_unrolled.json)
     asm volatile(
         "1:\n\t"
         "v_readlane_b32 %[t], %[va], %[X]\n\t"
@@ -492,32 +492,6 @@ __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vt
         "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
         "v_writelane_b32 %[vtin], %[t], m0\n\t"
         "s_cbranch_scc1 3f\n\t"
-        "v_readlane_b32 %[t], %[vb], %[X]\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
-        "v_writelane_b32 %[vtin], %[t], m0\n\t"
-        "s_cbranch_scc0 2b\n"
-        "3:"
-        : [vtin] "+v"(vtin), [X] "+s"(X), [t] "=&s"(t), [tmp] "=&s"(tmp), [h] "=&s"(half)
-        : [va] "v"(va), [vb] "v"(vb)
-        : "m0", "scc");
-    return;
-#endif
-    asm volatile(
-        "1:\n\t"
-        "v_readlane_b32 %[t], %[va], %[X]\n\t"
-        "s_lshr_b32 m0, %[X], 8\n\t"
-        "s_add_u32 %[X], %[t], %[X]\n\t"
-        "s_and_b32 %[tmp], %[X], 0x1c0c0\n\t"
-        "v_writelane_b32 %[vtin], %[t], m0\n\t"
-        "s_cbranch_scc0 1b\n\t"
-        "s_mov_b32 %[h], 0\n\t"
-        "s_and_b32 %[tmp], %[X], 0x1c080\n\t"
-        "s_cbranch_scc1 3f\n\t"
-        "s_sub_u32 %[X], %[X], 64\n\t"
-        "s_mov_b32 %[h], 64\n"
-        "2:\n\t"
         "v_readlane_b32 %[t], %[vb], %[X]\n\t"
         "s_lshr_b32 m0, %[X], 8\n\t"
         "s_add_u32 %[X], %[t], %[X]\n\t"
@@ -847,9 +821,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                     X = off << 8;
                     asm volatile("s_setprio 2");
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-                    #ifndef PPG_PRIO2
-                    asm volatile("s_setprio 1");   // (PPG_PRIO2: the emit stays at 2; A/B switch)
-#endif
+                                        asm volatile("s_setprio 1");
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -1009,26 +981,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         // (profiles/r04j_ab_pipelined_far.json).  (r02 tried the same on a kernel bound by SALU
         // issue: no gain.)
         auto hot_pipe = [&](uint32_t limh) -> uint32_t {
-#ifdef PPG_LEAN
             // no "pending" test: the loop starts with a dummy pending round (no far, no chain
             // sources) whose 64 garbage bytes land in the slots of positions [pos, pos + 64),
-            // which the first real round's finish overwrites before anything reads them
+            // which the first real round's finish overwrites before anything reads them; and no
+            // far-lane ballot: the far load is issued every round (97% of rounds have a far lane)
+            // -- together 567.5 -> 559.5 ms (profiles/r04o_ab_lean_unrolled.json)
             uint32_t p_val = 0, p_b = 0, p_pos = pos, lim_r;
             int32_t p_jj = -1;
-            constexpr bool pend = true;
-#else
-            uint32_t p_val = 0, p_b = 0, p_pos = 0, lim_r;
-            int32_t p_jj = 0;
-            uint64_t p_fm = 0;
-            bool pend = false;
-#endif
             auto finish = [&]() {
                 uint32_t val = p_val;
-#ifdef PPG_LEAN
                 val = p_jj < -(int32_t)(RING - 64) ? p_b : val;   // (no far lane: p_b unused)
-#else
-                if (p_fm) val = p_jj < -(int32_t)(RING - 64) ? p_b : val;
-#endif
                 const bool dep = p_jj >= 0;
                 if (__ballot(dep)) {
                     int32_t ptr = dep ? p_jj : lane;
@@ -1049,7 +1011,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 uint32_t sj4;
                 asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
                 const uint32_t inf = bperm(sj4, R.vtin);
-                if (pend) finish();
+                finish();
                 // the next round's stream words after the finish: the finish's s_waitcnt vmcnt(0)
                 // (the compiler's, for the far load) would otherwise also wait for a stream DMA
                 // issued here -- an HBM miss every ~9 rounds (574.6 -> 569.2 ms with the lookup
@@ -1062,13 +1024,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 const bool far = jj < -(int32_t)(RING - 64);
                 // pos >= 32768: every far source is the flushed output; a compiler-tracked load (its
                 // s_waitcnt lands at the first use, in finish)
-#ifdef PPG_LEAN
-                p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];   // 97% of rounds have a far lane
-#else
-                p_fm = __ballot(far);
-                if (p_fm) p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
-                pend = true;
-#endif
+                p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
                 p_jj = jj;
                 p_pos = pos;
                 cn = R.off - rout;
