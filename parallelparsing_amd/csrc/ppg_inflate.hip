@@ -460,6 +460,35 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 // out because the compiler adds an s_cmp_eq 0 after each s_and (one more SALU per token, and SALU
 // issue is what bounds this kernel); one block for both spans (r04: 642.3 -> 638.8 ms per 50 GB
 // step, same box, profiles/r04v2_ab_walk2_cw0_prio.json).  t: the last token word walked.
+#ifdef PPG_WGRP
+// spec_token for both spans with the litlen reads grouped: both lookups, then one lgkmcnt(0) (the
+// compiler waits for each lookup on its own; a second explicit wait after the distance lookups
+// is scheduled past their uses and only adds one)
+template <int LBT>
+__device__ __forceinline__ void spec_token2(const uint32_t *lit, const uint32_t *dst, uint32_t loa, uint32_t hia,
+                                            uint32_t lob, uint32_t hib, uint32_t &ta, uint32_t &tb) {
+    const uint32_t ea = lit[loa & ((1u << LBT) - 1)], eb = lit[lob & ((1u << LBT) - 1)];
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    const uint32_t e2a = ea >> 8, e2b = eb >> 8;
+    const uint32_t ya = __builtin_amdgcn_alignbit(hia, loa, e2a), yb = __builtin_amdgcn_alignbit(hib, lob, e2b);
+    const uint32_t da = dst[ya & ((1u << DB) - 1)], db = dst[yb & ((1u << DB) - 1)];
+    uint32_t tkea, tkeb;
+    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(tkea) : "v"(__builtin_amdgcn_ubfe(loa, ea, e2a - ea)), "v"(e2a));
+    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(tkeb) : "v"(__builtin_amdgcn_ubfe(lob, eb, e2b - eb)), "v"(e2b));
+    auto fin = [](uint32_t e, uint32_t y, uint32_t d, uint32_t tke) {
+        const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(y, d, d >> 10);
+        const uint32_t tlen = tke + ((d >> 5) & 31) + (dm1 << 17);
+        const uint32_t lm = (uint32_t)((int32_t)(e << 25) >> 31);
+        const uint32_t sd = (uint32_t)((int32_t)d >> 31);
+        uint32_t t2, tok;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(t2) : "v"(sd), "v"(PPG_SPECIAL_TOKEN), "v"(tlen));
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tok) : "v"(lm), "v"(t2), "v"(e));
+        return tok;
+    };
+    ta = fin(ea, ya, da, tkea);
+    tb = fin(eb, yb, db, tkeb);
+}
+#endif
 __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vtin, uint32_t &X, uint32_t &t,
                                           uint32_t &half) {
     uint32_t tmp;   // (the order is the compiler's own hazard-clean one for these instructions)
@@ -797,10 +826,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 const uint32_t o = bp + (uint32_t)lane;
                 const uint32_t x0 = W.x0, x1 = W.x1, x2 = W.x2, x3 = W.x3, x4 = W.x4;
                 // speculative tokens at every bit offset of the 128-bit span (two per lane)
+#ifdef PPG_WGRP
+                uint32_t vta, vtb;
+                spec_token2<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o), __builtin_amdgcn_alignbit(x2, x1, o),
+                                 __builtin_amdgcn_alignbit(x3, x2, o), __builtin_amdgcn_alignbit(x4, x3, o), vta, vtb);
+#else
                 const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
                                                      __builtin_amdgcn_alignbit(x2, x1, o), (uint32_t)lane);
                 const uint32_t vtb = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x3, x2, o),
                                                      __builtin_amdgcn_alignbit(x4, x3, o), (uint32_t)lane);
+#endif
 
                 // ---- walk the real token chain (wave-uniform): offset s -> s + bits(s) ----
                 // Each token goes to the lane of its output offset (vtin).  The walk state is one
@@ -819,9 +854,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
 #endif
                 if (HOT || len - pos >= 64) {
                     X = off << 8;
+#ifndef PPG_NOPRIO
                     asm volatile("s_setprio 2");
+#endif
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-                                        asm volatile("s_setprio 1");
+#ifndef PPG_NOPRIO
+                    asm volatile("s_setprio 1");
+#endif
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -1031,7 +1070,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 cw = R.tl & ~(511u << 8);
                 pos += rout;
                 bp += R.adv;
+#ifndef PPG_NOPRIO
                 asm volatile("s_setprio 0");
+#endif
                 lim_r = latch_limit(R.xr, limh);
             } while (pos < lim_r);
             finish();
