@@ -1029,7 +1029,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             int32_t p_jj = -1;
             auto finish = [&]() {
                 uint32_t val = p_val;
-                val = p_jj < -(int32_t)(RING - 64) ? p_b : val;   // (no far lane: p_b unused)
+                if constexpr (IX) {   // CreateIndex pass 1: the 16-bit symbol in the loaded dword
+                    const uint32_t q = 2u * ((p_pos + (uint32_t)p_jj) & IX_RING_MASK);
+                    val = p_jj < -(int32_t)(RING - 64) ? __builtin_amdgcn_ubfe(p_b, q << 3, 16u) : val;
+                } else {
+                    val = p_jj < -(int32_t)(RING - 64) ? p_b : val;   // (no far lane: p_b unused)
+                }
                 const bool dep = p_jj >= 0;
                 if (__ballot(dep)) {
                     int32_t ptr = dep ? p_jj : lane;
@@ -1059,11 +1064,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 W = words(bp + R.adv);
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
+                if constexpr (IX) p_val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
+                else p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
                 const bool far = jj < -(int32_t)(RING - 64);
                 // pos >= 32768: every far source is the flushed output; a compiler-tracked load (its
                 // s_waitcnt lands at the first use, in finish)
-                p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
+                if constexpr (IX) {   // the job's 64 Ki-symbol ring, as the dword holding the symbol
+                    const uint32_t q = 2u * ((pos + (uint32_t)jj) & IX_RING_MASK);
+                    p_b = *(const uint32_t *)(ob + (uint64_t)(far ? (q & ~3u) : 0u));
+                } else {
+                    p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
+                }
                 p_jj = jj;
                 p_pos = pos;
                 cn = R.off - rout;
@@ -1074,6 +1085,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 asm volatile("s_setprio 0");
 #endif
                 lim_r = latch_limit(R.xr, limh);
+                if constexpr (IX) {   // past the member, or runaway output (a false start)
+                    if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; lim_r = 0; }
+                }
             } while (pos < lim_r);
             finish();
             return lim_r;
@@ -1091,7 +1105,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             {
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
                 if (pos >= 32768u && pos < limh) {
+#ifdef PPG_IXPIPE
+                  if constexpr (true) {
+#else
                   if constexpr (!IX) {
+#endif
                     lim_r = hot_pipe(limh);
                   } else {
                     do {
