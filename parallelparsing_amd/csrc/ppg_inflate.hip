@@ -1105,17 +1105,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             {
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
                 if (pos >= 32768u && pos < limh) {
-#ifdef PPG_IXPIPE
-                  if constexpr (true) {
-#else
-                  if constexpr (!IX) {
-#endif
+                    // DecompressAll and CreateIndex pass 1 (r04: pass 1 792 -> 671 ms per 50 GB member,
+                    // profiles/r04q/)
                     lim_r = hot_pipe(limh);
-                  } else {
-                    do {
-                        lim_r = latch_limit(one_round(std::true_type{}), limh);
-                    } while (pos < lim_r);
-                  }
                     spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
                 }
                 if (!spec_ && pos < lim) {
