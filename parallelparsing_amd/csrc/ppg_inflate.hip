@@ -1019,7 +1019,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         // walk: 640.8 -> 575.8 ms per 50 GB step in one same-box A/B
         // (profiles/r04j_ab_pipelined_far.json).  (r02 tried the same on a kernel bound by SALU
         // issue: no gain.)
-        auto hot_pipe = [&](uint32_t limh) -> uint32_t {
+        // EARLY: the rounds of the chunk's (or piece's) first 32 KiB, where a far source may lie in the
+        // Point's window (p < 0): its byte comes from the window (DecompressAll: a per-lane address
+        // select) or is the history symbol itself (CreateIndex pass 1)
+        auto hot_pipe = [&](auto early, uint32_t limh) -> uint32_t {
+            constexpr bool EARLY = decltype(early)::value;
             // no "pending" test: the loop starts with a dummy pending round (no far, no chain
             // sources) whose 64 garbage bytes land in the slots of positions [pos, pos + 64),
             // which the first real round's finish overwrites before anything reads them; and no
@@ -1031,7 +1035,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 uint32_t val = p_val;
                 if constexpr (IX) {   // CreateIndex pass 1: the 16-bit symbol in the loaded dword
                     const uint32_t q = 2u * ((p_pos + (uint32_t)p_jj) & IX_RING_MASK);
-                    val = p_jj < -(int32_t)(RING - 64) ? __builtin_amdgcn_ubfe(p_b, q << 3, 16u) : val;
+                    uint32_t fv = __builtin_amdgcn_ubfe(p_b, q << 3, 16u);
+                    if constexpr (EARLY) {   // before the piece: the history symbol itself
+                        const int32_t p = (int32_t)p_pos + p_jj;
+                        fv = p < 0 ? 32768u + (uint32_t)p : fv;
+                    }
+                    val = p_jj < -(int32_t)(RING - 64) ? fv : val;
                 } else {
                     val = p_jj < -(int32_t)(RING - 64) ? p_b : val;   // (no far lane: p_b unused)
                 }
@@ -1071,7 +1080,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 // s_waitcnt lands at the first use, in finish)
                 if constexpr (IX) {   // the job's 64 Ki-symbol ring, as the dword holding the symbol
                     const uint32_t q = 2u * ((pos + (uint32_t)jj) & IX_RING_MASK);
-                    p_b = *(const uint32_t *)(ob + (uint64_t)(far ? (q & ~3u) : 0u));
+                    const bool ld = EARLY ? far && (int32_t)pos + jj >= 0 : far;
+                    p_b = *(const uint32_t *)(ob + (uint64_t)(ld ? (q & ~3u) : 0u));
+                } else if constexpr (EARLY) {
+                    // the flushed output (p >= 0) or the Point's window (p >= -32768)
+                    const int32_t p = (int32_t)pos + jj;
+                    const uint8_t *src = p >= 0 ? ob + (oa + (uint32_t)p) : dict + (uint32_t)(32768 + p);
+                    p_b = *(far ? src : ob);
                 } else {
                     p_b = ob[(uint64_t)(far ? (uint32_t)jj + (pos + oa) : 0u)];
                 }
@@ -1104,10 +1119,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             uint32_t lim_r;
             {
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
+#ifdef PPG_EARLYPIPE
+                if (pos < 32768u && pos < limh) {
+                    const uint32_t lime = min(limh, 32768u);
+                    lim_r = hot_pipe(std::true_type{}, lime);
+                    spec_ = lim_r == 0u;   // lime > pos >= 0 otherwise
+                }
+                if (!spec_ && pos >= 32768u && pos < limh) {
+#else
                 if (pos >= 32768u && pos < limh) {
+#endif
                     // DecompressAll and CreateIndex pass 1 (r04: pass 1 792 -> 671 ms per 50 GB member,
                     // profiles/r04q/)
-                    lim_r = hot_pipe(limh);
+                    lim_r = hot_pipe(std::false_type{}, limh);
                     spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
                 }
                 if (!spec_ && pos < lim) {
