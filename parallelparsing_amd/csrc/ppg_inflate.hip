@@ -1119,16 +1119,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             uint32_t lim_r;
             {
                 const uint32_t limh = min(fl_next, len > 322u ? len - 322u : 0u);
-#ifdef PPG_EARLYPIPE
+                // the first 32 KiB of a chunk or piece (far sources may lie in the Point's window):
+                // the same pipelined loop with a per-lane source select (r04: the N = 8 / 4 shares
+                // 74.17 -> 73.58 / 144.95 -> 143.65 ms, N = 1 unchanged; profiles/r04r/)
                 if (pos < 32768u && pos < limh) {
                     const uint32_t lime = min(limh, 32768u);
                     lim_r = hot_pipe(std::true_type{}, lime);
                     spec_ = lim_r == 0u;   // lime > pos >= 0 otherwise
                 }
                 if (!spec_ && pos >= 32768u && pos < limh) {
-#else
-                if (pos >= 32768u && pos < limh) {
-#endif
                     // DecompressAll and CreateIndex pass 1 (r04: pass 1 792 -> 671 ms per 50 GB member,
                     // profiles/r04q/)
                     lim_r = hot_pipe(std::false_type{}, limh);
