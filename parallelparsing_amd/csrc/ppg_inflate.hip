@@ -460,35 +460,6 @@ __device__ __forceinline__ uint32_t spec_token(const uint32_t *lit, const uint32
 // out because the compiler adds an s_cmp_eq 0 after each s_and (one more SALU per token, and SALU
 // issue is what bounds this kernel); one block for both spans (r04: 642.3 -> 638.8 ms per 50 GB
 // step, same box, profiles/r04v2_ab_walk2_cw0_prio.json).  t: the last token word walked.
-#ifdef PPG_WGRP
-// spec_token for both spans with the litlen reads grouped: both lookups, then one lgkmcnt(0) (the
-// compiler waits for each lookup on its own; a second explicit wait after the distance lookups
-// is scheduled past their uses and only adds one)
-template <int LBT>
-__device__ __forceinline__ void spec_token2(const uint32_t *lit, const uint32_t *dst, uint32_t loa, uint32_t hia,
-                                            uint32_t lob, uint32_t hib, uint32_t &ta, uint32_t &tb) {
-    const uint32_t ea = lit[loa & ((1u << LBT) - 1)], eb = lit[lob & ((1u << LBT) - 1)];
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-    const uint32_t e2a = ea >> 8, e2b = eb >> 8;
-    const uint32_t ya = __builtin_amdgcn_alignbit(hia, loa, e2a), yb = __builtin_amdgcn_alignbit(hib, lob, e2b);
-    const uint32_t da = dst[ya & ((1u << DB) - 1)], db = dst[yb & ((1u << DB) - 1)];
-    uint32_t tkea, tkeb;
-    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(tkea) : "v"(__builtin_amdgcn_ubfe(loa, ea, e2a - ea)), "v"(e2a));
-    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(tkeb) : "v"(__builtin_amdgcn_ubfe(lob, eb, e2b - eb)), "v"(e2b));
-    auto fin = [](uint32_t e, uint32_t y, uint32_t d, uint32_t tke) {
-        const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(y, d, d >> 10);
-        const uint32_t tlen = tke + ((d >> 5) & 31) + (dm1 << 17);
-        const uint32_t lm = (uint32_t)((int32_t)(e << 25) >> 31);
-        const uint32_t sd = (uint32_t)((int32_t)d >> 31);
-        uint32_t t2, tok;
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(t2) : "v"(sd), "v"(PPG_SPECIAL_TOKEN), "v"(tlen));
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tok) : "v"(lm), "v"(t2), "v"(e));
-        return tok;
-    };
-    ta = fin(ea, ya, da, tkea);
-    tb = fin(eb, yb, db, tkeb);
-}
-#endif
 __device__ __forceinline__ void walk2_asm(uint32_t va, uint32_t vb, uint32_t &vtin, uint32_t &X, uint32_t &t,
                                           uint32_t &half) {
     uint32_t tmp;   // (the order is the compiler's own hazard-clean one for these instructions)
@@ -826,16 +797,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 const uint32_t o = bp + (uint32_t)lane;
                 const uint32_t x0 = W.x0, x1 = W.x1, x2 = W.x2, x3 = W.x3, x4 = W.x4;
                 // speculative tokens at every bit offset of the 128-bit span (two per lane)
-#ifdef PPG_WGRP
-                uint32_t vta, vtb;
-                spec_token2<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o), __builtin_amdgcn_alignbit(x2, x1, o),
-                                 __builtin_amdgcn_alignbit(x3, x2, o), __builtin_amdgcn_alignbit(x4, x3, o), vta, vtb);
-#else
                 const uint32_t vta = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x1, x0, o),
                                                      __builtin_amdgcn_alignbit(x2, x1, o), (uint32_t)lane);
                 const uint32_t vtb = spec_token<LBT>(S.lit, S.dst, __builtin_amdgcn_alignbit(x3, x2, o),
                                                      __builtin_amdgcn_alignbit(x4, x3, o), (uint32_t)lane);
-#endif
 
                 // ---- walk the real token chain (wave-uniform): offset s -> s + bits(s) ----
                 // Each token goes to the lane of its output offset (vtin).  The walk state is one
@@ -854,13 +819,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
 #endif
                 if (HOT || len - pos >= 64) {
                     X = off << 8;
-#ifndef PPG_NOPRIO
                     asm volatile("s_setprio 2");
-#endif
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-#ifndef PPG_NOPRIO
                     asm volatile("s_setprio 1");
-#endif
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -892,10 +853,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         Words W = words(bp);
         // One round: decode + walk, then one output byte per lane.  Returns the walk's final state
         // (bit 7: a special token ended the round).
-        auto one_round = [&](auto hot) -> uint32_t {
-            constexpr bool HOT = decltype(hot)::value;
+        // The general form of a round (the last 322 bytes of a chunk or piece, short chunks): the
+        // round's far load waited for in the round.  The PPG_STAMPS / PPG_STATS diagnostics
+        // instrument this form only (r04: every other round runs hot_pipe below).
+        auto one_round = [&]() -> uint32_t {
+            constexpr bool HOT = false;
             PPG_STAMP(t0);
-            const Round R = decode(hot, bp, cn, cw, pos, W);
+            const Round R = decode(std::false_type{}, bp, cn, cw, pos, W);
             // the next round's stream words, read now: their LDS latency overlaps this round's
             // emit instead of opening the next round's chain of dependent LDS reads (r03)
             st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
@@ -1096,9 +1060,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 cw = R.tl & ~(511u << 8);
                 pos += rout;
                 bp += R.adv;
-#ifndef PPG_NOPRIO
                 asm volatile("s_setprio 0");
-#endif
                 lim_r = latch_limit(R.xr, limh);
                 if constexpr (IX) {   // past the member, or runaway output (a false start)
                     if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; lim_r = 0; }
@@ -1110,10 +1072,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         for (;;) {
             // The rounds up to the next flush boundary (or the output's end) as inner loops with ONE
             // latch each: pos < lim_r, where lim_r = 0 once a special token ended a round
-            // (latch_limit), so one compare leaves the rounds for all three reasons.  The HOT loop
-            // runs the rounds at least 32 KiB into the chunk and 322 bytes before its end; the
-            // general form the others.  (r04: 679.2 -> 641.8 ms per 50 GB step in one same-box A/B,
-            // profiles/r04_ab_round_control.json.)
+            // (latch_limit), so one compare leaves the rounds for all three reasons.  The pipelined
+            // loop (hot_pipe) runs every round at least 322 bytes before the chunk's end -- its
+            // EARLY form those of the first 32 KiB --; the general form (one_round) the others.
+            // (r04: 679.2 -> 641.8 ms per 50 GB step for the round control, then 640.8 -> 552.8 ms
+            // for the pipelining; profiles/r04_ab_round_control.json, r04j_*, r04l_*, r04o_*, r04r/.)
             bool spec_ = false;
             const uint32_t lim = min(len, fl_next);
             uint32_t lim_r;
@@ -1135,7 +1098,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 }
                 if (!spec_ && pos < lim) {
                     do {
-                        lim_r = latch_limit(one_round(std::false_type{}), lim);
+                        lim_r = latch_limit(one_round(), lim);
                     } while (pos < lim_r);
                     spec_ = lim_r == 0u;
                 }
