@@ -94,7 +94,7 @@ __device__ bool header_ok(const uint32_t *comp, uint64_t nwords, uint64_t c, Fin
 }  // namespace
 
 // cand[k] = the first bit b in [lo[k], hi[k]) where a dynamic Huffman block header zlib would
-// accept starts, or ~0.  Prefilter per lane: BTYPE = 2, HLIT <= 29, HDIST <= 29 and a complete
+// accept starts, or ~0.  Prefilter per lane: BFINAL = 0, BTYPE = 2, HLIT <= 29, HDIST <= 29 and a complete
 // code-length code (Kraft sum exactly 1); survivors get the full header_ok check, lowest first.
 __global__ __launch_bounds__(64) void ppg_block_find_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                             const uint64_t *__restrict__ lo,
@@ -115,7 +115,10 @@ __global__ __launch_bounds__(64) void ppg_block_find_kernel(const uint32_t *__re
         const uint32_t v1 = __builtin_amdgcn_alignbit(x2, x1, sh);
         const uint32_t v2 = __builtin_amdgcn_alignbit(x3, x2, sh);
         const uint64_t u01 = ((uint64_t)v1 << 32) | v0, u12 = ((uint64_t)v2 << 32) | v1;
-        bool ok = bit < b && ((v0 >> 1) & 3) == 2 && ((v0 >> 3) & 31) <= 29 && ((v0 >> 8) & 31) <= 29;
+        // BFINAL = 0: an inner block start is never the member's last block (missing that one only
+        // lengthens the piece before it), and the bit halves the survivors of the prefilter, whose
+        // serial header_ok checks are what the scan spends its time on
+        bool ok = bit < b && (v0 & 7) == 4 && ((v0 >> 3) & 31) <= 29 && ((v0 >> 8) & 31) <= 29;
         const uint32_t ncl = ((v0 >> 13) & 15) + 4;
         uint32_t kraft = 0;
 #pragma unroll
