@@ -406,10 +406,12 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
     t = Clock::now();
     int redo1 = 0;
     // the first piece after piece j's last block end E: pieces starting inside that block are false
-    // starts and are dropped
+    // starts and are dropped, except the last one before E's successor -- or the member's last
+    // piece, when no piece starts at or past E (the finder never offers the final block, whose
+    // start is not an inner one) -- which is redone from E
     auto next_piece = [&](size_t j, uint64_t E) {
         size_t k = j + 1;
-        while (k < pieces.size() && pieces[k].start < E && (k + 1 >= pieces.size() || pieces[k + 1].start <= E)) k++;
+        while (k + 1 < pieces.size() && pieces[k].start < E && pieces[k + 1].start <= E) k++;
         return k;
     };
     // Speculative redos, one launch: every piece k whose predecessor j (if real) ends somewhere
