@@ -42,23 +42,62 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def shared_tiled(args, key, build):
+def free_bytes(path):
+    """Bytes an unprivileged writer can still put under `path` (statvfs f_bavail), or -1."""
+    try:
+        st = os.statvfs(path)
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return -1
+
+
+def share_dir(preferred, need):
+    """Where local rank 0 publishes the input member for the other ranks: `preferred` (--shm-dir,
+    /dev/shm by default) when it has room for `need` bytes plus 10% and 1 GiB, else the first of
+    $TMPDIR, /tmp, /var/tmp that has (disk-backed: the ranks memory-map it from the page cache).
+    VERDICT r04: /dev/shm on the 8-GPU node may be smaller than the ~5 GB the 50 GB member's
+    description takes, and configs[3]'s first run would fail in setup.  Returns (dir, note)."""
+    want = int(need * 1.1) + (1 << 30)
+    cands = [preferred] + [d for d in (os.environ.get("TMPDIR"), "/tmp", "/var/tmp") if d and d != preferred]
+    for d in cands:
+        if os.path.isdir(d) and os.access(d, os.W_OK) and free_bytes(d) >= want:
+            return d, (None if d == preferred else
+                       f"{preferred} has {free_bytes(preferred) / 2**30:.1f} GiB free, {want / 2**30:.1f} GiB needed: "
+                       f"fell back to {d}")
+    raise OSError(f"no directory among {cands} has {want / 2**30:.1f} GiB free for the shared input "
+                  f"({', '.join(f'{d}: {free_bytes(d) / 2**30:.1f} GiB' for d in cands)})")
+
+
+def shared_tiled(args, key, build, need):
     """The synthetic member, built once per node: at N = 1 in this process; at N > 1 local rank 0
     builds it and saves it under /dev/shm (TiledFile.save), the other ranks memory-map that copy
     (TiledFile.load) instead of each rebuilding the ~4 GB text segment and deflating it (22 s and
-    ~5 GB of host RAM per rank, VERDICT r02 weak #4).  Returns (TiledFile, seconds, how)."""
+    ~5 GB of host RAM per rank).  `need`: the bytes the save takes (checked
+    against the directory's free space first: share_dir).  Returns (TiledFile, seconds, how)."""
     from parallelparsing_amd.tiled import TiledFile
     t = time.time()
     if args.world == 1:
         return build(), time.time() - t, "built"
     # a name no earlier (crashed) run can have left behind: a nonce from rank 0, broadcast (ADVICE
-    # r03: a stale 'ready' of a deterministic name let ranks map files being rewritten)
+    # r03: a stale 'ready' of a deterministic name let ranks map files being rewritten); rank 0
+    # also picks the directory (free space), so every rank looks in the same place
     import hashlib
     import uuid
     import torch.distributed as dist
-    nonce = [uuid.uuid4().hex if dist.get_rank() == 0 else None]
-    dist.broadcast_object_list(nonce, 0)
-    d = os.path.join(args.shm_dir, "ppg_bench_" + hashlib.sha1(repr((nonce[0], key)).encode()).hexdigest()[:12])
+    pick = [None, None, None]
+    if dist.get_rank() == 0:
+        try:
+            pick = [uuid.uuid4().hex, *share_dir(args.shm_dir, need)]
+        except OSError as e:
+            pick = [None, None, str(e)]
+    dist.broadcast_object_list(pick, 0)
+    nonce, base, note = pick
+    if nonce is None:
+        raise OSError(note)
+    if note:
+        log(f"[bench] {note}")
+    args.share_note = note
+    d = os.path.join(base, "ppg_bench_" + hashlib.sha1(repr((nonce, key)).encode()).hexdigest()[:12])
     args.shm_paths.append(d)
     if args.local_rank == 0:
         tf = build()
@@ -107,7 +146,9 @@ def build_input(args):
     else:  # 1m: configs[1], one non-repeated 1 M-read member
         key = ("1m", args.chunk)
         build = lambda: TiledFile(1_000_000, 1, args.chunk, threads=args.host_threads)   # noqa: E731
-    tf, sec, how = shared_tiled(args, key, build)
+    from parallelparsing_amd.tiled import saved_bytes_estimate
+    recs = args.seg_records if args.workload == "50gb" else 1_000_000
+    tf, sec, how = shared_tiled(args, key, build, saved_bytes_estimate(recs, blank_lines=args.blank_lines))
     args.input_seconds, args.input_how = sec, how
     log(f"[bench] input: {tf.records * tf.repeats:,} records, {tf.text_len * tf.repeats / 1e9:.1f} GB text, "
         f"{tf.file_len / 1e9:.2f} GB gz, {tf.npoints - 1} chunks, {how} in {sec:.1f}s")
@@ -469,9 +510,11 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
     from parallelparsing_amd.tiled import TiledFile
     reps = args.paired_repeats or 102
     t = time.time()
+    from parallelparsing_amd.tiled import saved_bytes_estimate
     tfs = [shared_tiled(args, ("paired", args.seg_records, reps, m),
                         lambda m=m: TiledFile(args.seg_records, reps, 50_000, seed=m - 1, mate=m,
-                                              threads=args.host_threads))[0]
+                                              threads=args.host_threads),
+                        saved_bytes_estimate(args.seg_records, mate=m))[0]
            for m in (1, 2)]
     args.input_seconds = time.time() - t
     log(f"[bench] paired input: 2 x {tfs[0].records * tfs[0].repeats:,} records, "
@@ -983,7 +1026,8 @@ def main():
         "build": build,
         # seconds per rank before timing: the input member ready (built once per node, shared via
         # /dev/shm for N > 1), then the rank's shard resident in HBM (compressed range, windows)
-        "setup_s": {"input_how": args.input_how, "per_rank": [{"input": round(x, 2), "shard": round(y, 2)}
+        "setup_s": {"input_how": args.input_how, **({"share_dir_note": args.share_note} if getattr(args, "share_note", None) else {}),
+                    "per_rank": [{"input": round(x, 2), "shard": round(y, 2)}
                                                                for x, y in setup_ranks]},
     }
     args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines and args.share == 1

@@ -128,6 +128,25 @@ void side_points_of(const ppg_index *ix, int32_t k, uint64_t job_bit, int64_t ou
     }
 }
 
+// The index's side points of chunk k lie strictly inside it in both output and compressed bits
+// (side_points_of selects them by output).  Checked per request before the launch is built, so a bad
+// side point fails only its own request, never the others sharing the launch (one bad
+// point made ppg_shard_set_split fail the whole launch).
+bool side_points_inside(const ppg_index *ix, int32_t k) {
+    const auto &O = ix->side_out;
+    if (O.empty()) return true;
+    const PpgPoint &from = ix->pts[(size_t)k], &to = ix->pts[(size_t)k + 1];
+    const int64_t from_bit = 8 * from.input - from.bits, to_bit = 8 * to.input - to.bits;
+    const size_t a = (size_t)(std::upper_bound(O.begin(), O.end(), from.output) - O.begin());
+    const size_t b = (size_t)(std::lower_bound(O.begin(), O.end(), to.output) - O.begin());
+    int64_t prev = from_bit;
+    for (size_t q = a; q < b; q++) {
+        if (ix->side_bit[q] <= prev || ix->side_bit[q] >= to_bit) return false;
+        prev = ix->side_bit[q];
+    }
+    return true;
+}
+
 // Side points for chunks whose index has none (a .gzi carries only the Points): the inner deflate
 // block starts of each chunk found on the GPU the way the GPU CreateIndex finds them
 // (ppg_index_gpu.cpp) -- candidate dynamic-block headers every ~1/16 of the chunk's compressed bytes
@@ -323,6 +342,7 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
         int rc = ppg_index_validate(r->ix, r->k, 1);
         if (rc == PPG_OK && r->slice_len != P[(size_t)r->k + 1].input - P[(size_t)r->k].input + 1) rc = PPG_ARG_ERROR;
         if (rc == PPG_OK && r->ix->windows.size() < ((size_t)r->k + 1) * kWin) rc = PPG_ARG_ERROR;
+        if (rc == PPG_OK && !side_points_inside(r->ix, r->k)) rc = PPG_ARG_ERROR;
         if (rc != PPG_OK) {
             r->rc = rc;
             continue;
@@ -459,7 +479,14 @@ int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uin
         svc->launches++;
         svc->max_batch = std::max<int64_t>(svc->max_batch, (int64_t)batch.size());
         lk.unlock();
-        const int rc = run_launch(ctx, *svc, sl, batch);
+        int rc;
+        try {
+            rc = run_launch(ctx, *svc, sl, batch);
+        } catch (const std::bad_alloc &) {   // host vectors: never out through the C ABI, never a stuck slot
+            rc = PPG_MEM_ERROR;
+        } catch (...) {
+            rc = PPG_DEVICE_ERROR;
+        }
         lk.lock();
         for (ChunkReq *r : batch) {
             if (rc != PPG_OK) r->rc = rc;

@@ -470,6 +470,42 @@ int comm_all_gather_i64(ppg_comm *c, const int64_t *send, int64_t *recv, size_t 
 // point-to-point); host transport: staged through host memory in rounds of the shared slots.
 // The caller's stream s must have produced `send` (it is synchronised first).  Every rank runs
 // every round whatever its own errors (the others would wait); the first error is returned after.
+// The grouped ncclSend / ncclRecv of one all-to-all-v, with the group ALWAYS closed: a send or recv
+// that fails to enqueue stops further enqueues, but ncclGroupEnd still runs, so this rank neither
+// leaves a group open on its thread (the next collective on the comm would misbehave instead of
+// failing) nor returns before the group's launch.  The first error is returned.  The
+// RCCL entry points come in as a table so host_check can drive the error paths without a GPU.
+int comm_grouped_p2p(const CommP2P &f, void *comm, hipStream_t stream, const int64_t *send, int64_t *recv,
+                     const int64_t *m, int32_t R, int32_t me, const int64_t *sd, const int64_t *rd) {
+    ncclResult_t first = f.group_start();
+    if (first != ncclSuccess) {
+        fprintf(stderr, "ppgpu: ncclGroupStart failed: %s\n", f.err ? f.err(first) : "?");
+        return PPG_DEVICE_ERROR;   // no group was opened
+    }
+    const char *what = nullptr;
+    for (int32_t q = 0; q < R && first == ncclSuccess; q++) {
+        if (q == me) continue;
+        if (m[(size_t)me * R + q]) {
+            first = f.send(send + sd[q], (size_t)m[(size_t)me * R + q], ncclInt64, q, (ncclComm_t)comm, stream);
+            what = "ncclSend";
+        }
+        if (first == ncclSuccess && m[(size_t)q * R + me]) {
+            first = f.recv(recv + rd[q], (size_t)m[(size_t)q * R + me], ncclInt64, q, (ncclComm_t)comm, stream);
+            what = "ncclRecv";
+        }
+    }
+    const ncclResult_t end = f.group_end();
+    if (first != ncclSuccess) {
+        fprintf(stderr, "ppgpu: %s failed: %s\n", what, f.err ? f.err(first) : "?");
+        return PPG_DEVICE_ERROR;
+    }
+    if (end != ncclSuccess) {
+        fprintf(stderr, "ppgpu: ncclGroupEnd failed: %s\n", f.err ? f.err(end) : "?");
+        return PPG_DEVICE_ERROR;
+    }
+    return PPG_OK;
+}
+
 int comm_alltoallv_i64(ppg_comm *c, hipStream_t s, const int64_t *send, int64_t *recv, const int64_t *m,
                        bool on_device) {
     const int32_t R = c->nranks, me = c->rank;
@@ -483,15 +519,8 @@ int comm_alltoallv_i64(ppg_comm *c, hipStream_t s, const int64_t *send, int64_t 
         if (!on_device) return PPG_ARG_ERROR;   // RCCL moves device memory only
         if (!rccl().send || !rccl().recv || !rccl().group_start || !rccl().group_end) return PPG_UNSUPPORTED;
         HIPCHK(hipSetDevice(c->device));
-        RCCLCHK(rccl().group_start());
-        for (int32_t q = 0; q < R; q++) {
-            if (q == me) continue;
-            if (m[(size_t)me * R + q])
-                RCCLCHK(rccl().send(send + sd[(size_t)q], (size_t)m[(size_t)me * R + q], ncclInt64, q, c->nccl, c->stream));
-            if (m[(size_t)q * R + me])
-                RCCLCHK(rccl().recv(recv + rd[(size_t)q], (size_t)m[(size_t)q * R + me], ncclInt64, q, c->nccl, c->stream));
-        }
-        RCCLCHK(rccl().group_end());
+        const CommP2P f{rccl().send, rccl().recv, rccl().group_start, rccl().group_end, rccl().err};
+        if (int g = comm_grouped_p2p(f, c->nccl, c->stream, send, recv, m, R, me, sd.data(), rd.data())) return g;
         if (m[(size_t)me * R + me])
             HIPCHK(hipMemcpyAsync(recv + rd[(size_t)me], send + sd[(size_t)me], 8 * (size_t)m[(size_t)me * R + me],
                                   hipMemcpyDeviceToDevice, c->stream));

@@ -2,6 +2,7 @@
 // (ppg_api.cpp: C ABI, index I/O, shards, ingest; ppg_index_gpu.cpp: GPU CreateIndex).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -221,3 +222,13 @@ int comm_device(const ppg_comm *c);   // -1: host transport
 int comm_all_gather_i64(ppg_comm *c, const int64_t *send, int64_t *recv, size_t n, bool &sent_ok);
 int comm_alltoallv_i64(ppg_comm *c, hipStream_t s, const int64_t *send, int64_t *recv, const int64_t *m,
                        bool on_device);
+// the RCCL point-to-point entry points of one grouped exchange (ppg_comm.cpp; host_check passes fakes)
+struct CommP2P {
+    ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*group_start)();
+    ncclResult_t (*group_end)();
+    const char *(*err)(ncclResult_t);
+};
+int comm_grouped_p2p(const CommP2P &f, void *comm, hipStream_t stream, const int64_t *send, int64_t *recv,
+                     const int64_t *m, int32_t R, int32_t me, const int64_t *sd, const int64_t *rd);

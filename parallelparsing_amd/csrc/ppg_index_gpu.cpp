@@ -344,6 +344,16 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         for (size_t i = 0; n > 0 && i < cand.size(); i++)
             if (i % (size_t)n == (size_t)n - 1 && cand[i] != ~0ull && cand[i] + 1 < end_bits) cand[i] += 1;
     }
+    if (getenv("PPG_IX_PERTURB_LAST")) {
+        // test hook: the LAST candidate moved one bit back, into the previous block --
+        // the member's last piece then starts inside its predecessor's last block, and next_piece
+        // must redo it from that block's end (tests/test_index_gpu.py)
+        for (size_t i = cand.size(); i-- > 0;)
+            if (cand[i] != ~0ull) {
+                if (cand[i] > d0 + 1) cand[i] -= 1;
+                break;
+            }
+    }
     std::vector<Piece> pieces{{0, d0}};
     for (uint64_t c : cand)
         if (c != ~0ull) pieces.push_back({(uint32_t)pieces.size(), c});
@@ -924,6 +934,16 @@ int ppg_index_set_side_points(ppg_index *ix, int32_t n, const int64_t *bit, cons
     if (!ix || n < 0 || (n && (!bit || !output || !windows))) return PPG_ARG_ERROR;
     for (int32_t i = 1; i < n; i++)
         if (output[i] <= output[i - 1] || bit[i] <= bit[i - 1]) return PPG_ARG_ERROR;
+    // each point strictly inside one chunk of the index, in output AND in compressed bits (ADVICE
+    // r04: a point outside its chunk's bit range failed every request of a shared Decompress launch)
+    const auto &P = ix->pts;
+    if (n && P.size() < 2) return PPG_ARG_ERROR;
+    for (int32_t i = 0, c = 0; i < n; i++) {
+        while ((size_t)c + 1 < P.size() && output[i] >= P[(size_t)c + 1].output) c++;
+        if ((size_t)c + 1 >= P.size() || output[i] <= P[(size_t)c].output) return PPG_ARG_ERROR;
+        const int64_t b0 = 8 * P[(size_t)c].input - P[(size_t)c].bits, b1 = 8 * P[(size_t)c + 1].input - P[(size_t)c + 1].bits;
+        if (bit[i] <= b0 || bit[i] >= b1) return PPG_ARG_ERROR;
+    }
     ix->side_bit.assign(bit, bit + n);
     ix->side_out.assign(output, output + n);
     ix->side_win.resize((size_t)n * kWin);

@@ -81,7 +81,8 @@ __device__ unsigned long long ppg_ixstat[16];
 // diagnostic build only (EXTRA=-DPPG_STAMPS): s_memtime stamps at the phase boundaries of every
 // token round, summed per wave and added to these totals at the end of each chunk; the launcher
 // prints them (cycles per phase, rounds) after each launch.  Perturbs the schedule (+~10%).
-__device__ unsigned long long ppg_stamp_acc[8];
+// [0..7]: the general rounds (one_round); [8..15]: the pipelined rounds (hot_pipe, r05)
+__device__ unsigned long long ppg_stamp_acc[16];
 #define PPG_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #else
 #define PPG_STAMP(t)
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     uint32_t nblk = 0;
 #ifdef PPG_STAMPS
     uint64_t sa_dec = 0, sa_walk = 0, sa_rd = 0, sa_far = 0, sa_dep = 0, sa_tail = 0, sa_rounds = 0, sa_farr = 0;
+    uint64_t hs_dec = 0, hs_walk = 0, hs_look = 0, hs_fin = 0, hs_words = 0, hs_emit = 0, hs_rounds = 0;
 #endif
 #ifdef PPG_STATS
     // debug build only (EXTRA=-DPPG_STATS): per-chunk round / token / path counts, printed for the
@@ -1021,20 +1023,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 S.ring[(rb0 + p_pos + lane) & RM] = (RingT)val;
             };
             do {
+                PPG_STAMP(h0);
                 const Round R = decode(std::true_type{}, bp, cn, cw, pos, W);
+#ifdef PPG_STAMPS
+                const uint64_t h1 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(R.vtin);
+                if (st_w0 < h0) st_w0 = h1;   // no walk this round
+                hs_dec += st_w0 - h0;
+                hs_walk += h1 - st_w0;
+                hs_rounds++;
+#endif
                 // the token lookup does not read the ring: issued before the pending round's finish
                 const uint32_t rout = min(R.off, 64u);
                 const uint64_t mo = __ballot(R.vtin != 0);
                 uint32_t sj4;
                 asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
                 const uint32_t inf = bperm(sj4, R.vtin);
+#ifdef PPG_STAMPS
+                const uint64_t h2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(inf);
+                hs_look += h2 - h1;
+#endif
                 finish();
+#ifdef PPG_STAMPS
+                const uint64_t h3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(
+                                                                       S.ring[(rb0 + p_pos + lane) & RM]);
+                hs_fin += h3 - h2;
+#endif
                 // the next round's stream words after the finish: the finish's s_waitcnt vmcnt(0)
                 // (the compiler's, for the far load) would otherwise also wait for a stream DMA
                 // issued here -- an HBM miss every ~9 rounds (574.6 -> 569.2 ms with the lookup
                 // above, profiles/r04l_ab_pipeline_variants.json)
                 st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
                 W = words(bp + R.adv);
+#ifdef PPG_STAMPS
+                const uint64_t h4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(W.x4);
+                hs_words += h4 - h3;
+#endif
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 if constexpr (IX) p_val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
@@ -1065,6 +1088,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if constexpr (IX) {   // past the member, or runaway output (a false start)
                     if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; lim_r = 0; }
                 }
+#ifdef PPG_STAMPS
+                hs_emit += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(p_b + lim_r) - h4;
+                st_w0 = 0;
+#endif
             } while (pos < lim_r);
             finish();
             return lim_r;
@@ -1199,6 +1226,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         atomicAdd(&ppg_stamp_acc[5], (unsigned long long)sa_tail);
         atomicAdd(&ppg_stamp_acc[6], (unsigned long long)sa_rounds);
         atomicAdd(&ppg_stamp_acc[7], (unsigned long long)sa_farr);
+        atomicAdd(&ppg_stamp_acc[8], (unsigned long long)hs_dec);
+        atomicAdd(&ppg_stamp_acc[9], (unsigned long long)hs_walk);
+        atomicAdd(&ppg_stamp_acc[10], (unsigned long long)hs_look);
+        atomicAdd(&ppg_stamp_acc[11], (unsigned long long)hs_fin);
+        atomicAdd(&ppg_stamp_acc[12], (unsigned long long)hs_words);
+        atomicAdd(&ppg_stamp_acc[13], (unsigned long long)hs_emit);
+        atomicAdd(&ppg_stamp_acc[14], (unsigned long long)hs_rounds);
     }
 #endif
     if (lane == 0) {
@@ -1262,15 +1296,19 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
 // diagnostic build: print and reset the per-phase round totals (after the stream drains)
 struct PpgStampPrinter {
     static void dump(hipStream_t s) {
-        unsigned long long h[8] = {0};
+        unsigned long long h[16] = {0};
         if (hipStreamSynchronize(s) != hipSuccess) return;
         if (hipMemcpyFromSymbol(h, HIP_SYMBOL(ppg_stamp_acc), sizeof h) != hipSuccess) return;
-        const unsigned long long z[8] = {0};
+        const unsigned long long z[16] = {0};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(ppg_stamp_acc), z, sizeof z);
         const double r = h[6] ? (double)h[6] : 1.0;
         fprintf(stderr, "PPG_STAMPS rounds %llu far-rounds %llu cycles/round: decode %.1f walk %.1f read %.1f far %.1f "
                         "dep+write %.1f tail %.1f total %.1f\n", h[6], h[7], h[0] / r, h[1] / r, h[2] / r, h[3] / r,
                 h[4] / r, h[5] / r, (h[0] + h[1] + h[2] + h[3] + h[4] + h[5]) / r);
+        const double q = h[14] ? (double)h[14] : 1.0;
+        fprintf(stderr, "PPG_STAMPS hot rounds %llu cycles/round: decode %.1f walk %.1f lookup %.1f finish %.1f "
+                        "words %.1f emit+tail %.1f total %.1f\n", h[14], h[8] / q, h[9] / q, h[10] / q, h[11] / q,
+                h[12] / q, h[13] / q, (h[8] + h[9] + h[10] + h[11] + h[12] + h[13]) / q);
     }
 };
 #endif

@@ -15,6 +15,16 @@ from ._lib import synth
 from . import Index
 
 
+def saved_bytes_estimate(records, read_len=150, mate=0, blank_lines=False):
+    """Upper bound on what TiledFile.save writes for a member of `records`-record segments: the
+    segment text, its deflate (well under half the text at level 6), the block list and the points
+    (a few hundred bytes per chunk) -- for the free-space check of the directory it goes to."""
+    n = synth().ppg_synth_fastq_size_mate(0, records, read_len, mate)
+    if blank_lines:
+        n += records
+    return int(1.6 * n) + (64 << 20)
+
+
 class TiledFile:
     def __init__(self, records, repeats, chunksize, read_len=150, seed=0, level=6, piece=4 << 20, threads=16,
                  mate=0, blank_lines=False):

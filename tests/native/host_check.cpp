@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/ppgpu.h"
+#include "../../parallelparsing_amd/csrc/ppg_host.h"
 
 static std::atomic<int> failures{0};
 #define CHECK(c)                                                                  \
@@ -173,6 +174,51 @@ static void check_alltoallv(int world) {
     CHECK(ok == world);
 }
 
+// The RCCL grouped send/recv of ppg_comm_alltoallv with fake entry points (a failed
+// ncclSend / ncclRecv returned with the group still open).  Whichever call fails -- the k-th send or
+// recv, or ncclGroupEnd itself -- the group is closed exactly once, nothing is enqueued after the
+// failure, and the status is PPG_DEVICE_ERROR; a failed ncclGroupStart opens nothing.
+namespace fake_rccl {
+static int calls, fail_at, starts, ends, after_fail;
+static bool failed, fail_start, fail_end;
+static ncclResult_t step() {
+    if (failed) after_fail++;
+    if (++calls == fail_at) { failed = true; return ncclUnhandledCudaError; }
+    return ncclSuccess;
+}
+static ncclResult_t send(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) { return step(); }
+static ncclResult_t recv(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) { return step(); }
+static ncclResult_t gstart() { starts++; return fail_start ? ncclInternalError : ncclSuccess; }
+static ncclResult_t gend() { ends++; return fail_end ? ncclInternalError : ncclSuccess; }
+static const char *err(ncclResult_t) { return "fake"; }
+}  // namespace fake_rccl
+
+static void check_grouped_p2p() {
+    namespace F = fake_rccl;
+    const int32_t R = 4, me = 1;
+    std::vector<int64_t> m((size_t)R * R, 5), sd((size_t)R + 1), rd((size_t)R + 1);
+    for (int32_t q = 0; q < R; q++) {
+        sd[(size_t)q + 1] = sd[(size_t)q] + m[(size_t)me * R + q];
+        rd[(size_t)q + 1] = rd[(size_t)q] + m[(size_t)q * R + me];
+    }
+    std::vector<int64_t> snd((size_t)sd[R]), rcv((size_t)rd[R]);
+    const CommP2P f{F::send, F::recv, F::gstart, F::gend, F::err};
+    const int total = 2 * (R - 1);   // one send and one recv per peer
+    for (int mode = 0; mode <= total + 2; mode++) {
+        F::calls = F::starts = F::ends = F::after_fail = 0;
+        F::failed = false;
+        F::fail_at = mode >= 1 && mode <= total ? mode : 0;
+        F::fail_start = mode == total + 1;
+        F::fail_end = mode == total + 2;
+        const int rc = comm_grouped_p2p(f, nullptr, nullptr, snd.data(), rcv.data(), m.data(), R, me, sd.data(), rd.data());
+        CHECK(rc == (mode == 0 ? PPG_OK : PPG_DEVICE_ERROR));
+        CHECK(F::starts == 1);
+        CHECK(F::ends == (F::fail_start ? 0 : 1));      // always closed once, unless never opened
+        CHECK(F::after_fail == 0);                      // nothing enqueued after the failure
+        CHECK(F::calls == (F::fail_start ? 0 : F::fail_at ? F::fail_at : total));
+    }
+}
+
 int main(int argc, char **argv) {
     if (argc < 3) {
         fprintf(stderr, "usage: host_check <golden dir> <scratch dir>\n");
@@ -194,6 +240,7 @@ int main(int argc, char **argv) {
     }
     for (int world : {2, 3, 5}) check_comm(g + "/l6_c200.gz", 200, world, 4);
     for (int world : {2, 3}) check_alltoallv(world);
+    check_grouped_p2p();
     printf("host_check: %s (%d failures)\n", failures ? "FAILED" : "ok", failures.load());
     return failures ? 1 : 0;
 }

@@ -80,3 +80,30 @@ def test_gather_pairs_gloo_world2():
     for p in ps:
         p.join(60)
     assert got[0] == got[1] == [[0.0, 10.0], [1.0, 11.0]]
+
+
+def test_share_dir_falls_back_when_shm_is_small(monkeypatch, tmp_path):
+    """The shared input's directory (/dev/shm on the 8-GPU node may be smaller than the
+    ~6 GB the 50 GB member's description takes): --shm-dir when it has room, else $TMPDIR (then
+    /tmp, /var/tmp), with the reason in the line; no room anywhere is an OSError before any save."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from parallelparsing_amd.tiled import saved_bytes_estimate
+    need = saved_bytes_estimate(10_485_760)   # the default 50 GB member's segment
+    assert 4 << 30 < need < 8 << 30
+    shm, tmpd = str(tmp_path / "shm"), str(tmp_path / "tmp")
+    os.makedirs(shm)
+    os.makedirs(tmpd)
+    free = {shm: 2 << 30, tmpd: 100 << 30}
+    monkeypatch.setattr(bench, "free_bytes", lambda p: free.get(p, 0))
+    monkeypatch.setenv("TMPDIR", tmpd)
+    d, note = bench.share_dir(shm, need)
+    assert d == tmpd and note and "fell back" in note
+    free[shm] = 64 << 30
+    assert bench.share_dir(shm, need) == (shm, None)
+    free[shm] = free[tmpd] = 1 << 30
+    try:
+        bench.share_dir(shm, need)
+        raise AssertionError("no room anywhere must raise")
+    except OSError as e:
+        assert "GiB free" in str(e)

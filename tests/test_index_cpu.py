@@ -122,3 +122,28 @@ def test_host_create_index_rejects_bad_trailer_crc():
     with pytest.raises(pp.PpgError) as e:
         pp.Core.BuildDeflateIndex(bad, meta["chunksize"])
     assert e.value.code == -3
+
+
+def test_set_side_points_rejects_points_outside_their_chunk():
+    """ppg_index_set_side_points checks every side point against the Points: strictly inside one
+    chunk in output AND in compressed bits (a point outside its chunk's bit range made
+    a shared Decompress launch fail every request in it).  Valid points are accepted."""
+    meta, gz = load_case("l6_c200")
+    ix = pp.Core.BuildDeflateIndex(gz, meta["chunksize"])
+    assert ix.Count >= 3
+    o0, i0, b0, _ = ix.point_fields(0)
+    o1, i1, b1, _ = ix.point_fields(1)
+    o2, i2, b2, _ = ix.point_fields(2)
+    bit0, bit1, bit2 = 8 * i0 - b0, 8 * i1 - b1, 8 * i2 - b2
+    w = np.zeros(32768, np.uint8)
+    good = ((bit0 + bit1) // 2, (o0 + o1) // 2)
+    ix.set_side_points([good[0]], [good[1]], w)          # inside chunk 0 in both: accepted
+    bad = [((bit1 + bit2) // 2, good[1]),                # output in chunk 0, bits in chunk 1
+           (bit0, good[1]),                              # at chunk 0's own start bit
+           (bit1, good[1]),                              # at the next Point's bit
+           (good[0], o1),                                # output exactly at a Point
+           (good[0], o0 - 1 if o0 > 0 else -1)]          # before the first Point
+    for b, o in bad:
+        with pytest.raises(pp.PpgError) as e:
+            ix.set_side_points([b], [o], w)
+        assert e.value.code == pp._lib.PPG_ARG_ERROR, (b, o)

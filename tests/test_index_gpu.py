@@ -293,3 +293,20 @@ def test_false_start_redos_speculative_and_serial(spares, device, monkeypatch):
         assert total_spec == 0 and total_serial > 0
     elif spares == "":
         assert total_spec > 0
+
+
+@pytest.mark.parametrize("spares", ["0", ""])
+def test_last_piece_inside_previous_block_redone(spares, device, monkeypatch):
+    """The member's last piece starting inside the previous piece's last block (the
+    finder never offers the final block, so a false last candidate used to fail the chain): the
+    last finder candidate is moved one bit back into the block before it (PPG_IX_PERTURB_LAST),
+    and the chain walk redoes that piece from the block's end -- speculatively into a spare slot
+    or serially (PPG_IX_SPARES=0).  The Points equal the CPU CreateIndex's."""
+    monkeypatch.setenv("PPG_IX_SPARES", spares)
+    monkeypatch.setenv("PPG_IX_PERTURB_LAST", "1")
+    redone = 0
+    for name in CASES:
+        meta, gz = load_case(name)
+        _, st = check_both(gz, meta["chunksize"], device, piece_bytes=1024)
+        redone += st["redo1"]
+    assert redone > 0
