@@ -413,12 +413,29 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
         finally:
             os.environ.pop("PPG_CHUNK_NO_FIND", None)
 
+    def async_leg(ix, depth):
+        """One caller thread queues `depth` chunks (ppg_decompress_chunk_submit) and then takes the
+        results in order (ppg_decompress_chunk_wait)."""
+        n = min(nmax, depth)
+        before = dev.decompress_chunk_stats()
+        t = time.perf_counter()
+        futs = [pp.Core.ExtractDeflateIndexAsync(slices[k], ix, k, device=dev) for k in range(n)]
+        got = np.array([len(f.result()[2]) for f in futs], np.int64)
+        sec = time.perf_counter() - t
+        assert (got == counts[:n]).all(), "ppg_decompress_chunk_submit record counts differ from DecompressAll's"
+        after = dev.decompress_chunk_stats()
+        return {"chunks": n, "records_per_s": float(got.sum()) / sec, "chunks_per_s": n / sec, "seconds": sec,
+                "launches": after["launches"] - before["launches"]}
+
     leg(plain, 8)   # warm: the slots' buffers grow to their working size
     out = {f"T{T}": leg(plain, T) for T in threads_list}
+    async_leg(plain, 256)   # warm the launcher thread and the larger launches' buffers
+    out["async"] = {f"depth{d}": async_leg(plain, d) for d in (256, 1024)}
     out["no_find"] = {f"T{T}": no_find(T) for T in threads_list}
     out["side_points"] = {f"T{T}": leg(split, T) for T in threads_list}
     out["note"] = ("ppg_decompress_chunk from T host threads on one ctx (concurrent calls combined into shared "
-                   "launches, two launch slots); plain index: each chunk's inner block starts found on the GPU "
+                   "launches, four launch slots); async: one thread queues `depth` chunks (ppg_decompress_chunk_submit) "
+                   "then waits for each; plain index: each chunk's inner block starts found on the GPU "
                    "(<= 16 waves per chunk); no_find: one wave per chunk; side_points: the index's own, "
                    f"<= {side} waves per chunk (ppg_index_set_side_points); host slices in, bytes + descriptors out; "
                    "not the bench value")
@@ -556,7 +573,10 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
             raise RuntimeError(f"paired run needs the library's communicator: {via}")
         via = "ppg_pairs_check: keys to pair owners by ppg_comm_alltoallv (" + via.split(" over ")[-1] + ")"
 
-    def step():
+    K = args.pair_chunk
+    emit_ms = []
+
+    def step(emit=True):
         errs = []
 
         def run(sh):
@@ -574,7 +594,16 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
         res = pairs.check(shards[0], shards[1], comm)
         if errs:
             raise errs[0]
-        return paired.require_pairs(res)
+        n = paired.require_pairs(res)
+        if emit:
+            # the deliverable: every record-aligned pair chunk of this rank packed on the device
+            # (ppg_pairs_emit_*: one rank re-runs multi-batch shards window by window; N ranks move
+            # the mates' records to each pair chunk's owner), each window consumed before the next
+            t = time.perf_counter()
+            for _ in pairs.emit(shards[0], shards[1], K, comm, window_bytes=int(args.pair_window_gib * (1 << 30))):
+                pass
+            emit_ms.append((time.perf_counter() - t) * 1e3)
+        return n
 
     import torch.distributed as dist
     for _ in range(args.warmup):
@@ -595,8 +624,24 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
         elapsed = float(e.item())
     assert npairs == tfs[0].records * tfs[0].repeats, (npairs, tfs[0].records * tfs[0].repeats)
     text = sum(int(tf.p_output[-1] - tf.p_output[0]) for tf in tfs)
+    est = pairs.emit_stats()
+    emission = {"pair_chunk": K, "pair_chunks": est["pair_chunks"], "this_rank": list(est["mine"]) if world > 1 else None,
+                "ms_per_step": statistics.median(emit_ms[-args.steps:]) if emit_ms else None,
+                "last_step_ms": {k: round(est[k], 2) for k in ("rerun_ms", "pack_ms", "exchange_ms", "emit_ms")},
+                "batches_rerun_per_step": est["reruns"],
+                "verified": verify_pair_chunks(pairs, tfs, K, shards, comm, world, rank),
+                "note": "every pair chunk of this rank packed on the device per step (records back to back + "
+                        "descriptors per half, ppg_pairs_emit_*), inside the timed step; multi-batch shards on one "
+                        "GPU run their batches again as the windows advance"}
+    # the previous round's line (decode + check, no emission) for comparison, timed after the main loop
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step(emit=False)
+    torch.cuda.synchronize()
+    check_only = (time.perf_counter() - t1) / args.steps
     return {
-        "metric": f"paired-end record pairs/sec (R1+R2 DecompressAll + pair check), {world} MI355X",
+        "metric": f"paired-end record pairs/sec (R1+R2 DecompressAll + pair check + record-aligned pair chunks), "
+                  f"{world} MI355X",
         "value": npairs * args.steps / elapsed,
         "unit": "pairs/s",
         "n_gpus": world,
@@ -614,10 +659,56 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
                    "output_batches_per_file": [sh.batches for sh in shards],
                    "keys": "per output batch while resident (ppg_shard_set_keys)",
                    "pair_check": via,
+                   "pair_chunks": f"{K:,} pairs each, packed on the device (ppg_pairs_emit_*)",
                    "waves_per_chunk": f"<= {args.split} (side points)" if args.split > 1 else 1},
         "decompressed_MBps": text * args.steps / elapsed / 1e6,
         "setup_s": {"input": round(args.input_seconds, 2), "shards": round(setup_s, 2)},
+        "emission": emission,
+        "without_emission": {"pairs_per_s": npairs / check_only if world == 1 else None,
+                             "ms_per_step": check_only * 1e3,
+                             "note": "decode + pair check only (the r04 line), rank 0's own clock"},
     }
+
+
+def verify_pair_chunks(pairs, tfs, K, shards, comm, world, rank, samples=3):
+    """Spot-check emitted pair chunks against the tiled members' text (after the timed loop): a few
+    pair chunks of this rank -- the first, one straddling an output batch boundary when there is
+    one, the last -- copied to the host, each half's bytes and descriptors equal to records
+    [j*K, (j+1)*K) of its member (pair i = record i mod the segment's records of both files)."""
+    want = set()
+    for j0, j1 in pairs.emit(shards[0], shards[1], K, comm):
+        span = list(range(j0, j1))
+        pick = {span[0], span[-1], span[len(span) // 2]} if span else set()
+        for j in sorted(pick)[:samples]:
+            for f, tf in enumerate(tfs):
+                b, d = pairs.copy_chunk(j, f)
+                eb = tiled_records(tf, j * K, min((j + 1) * K, tf.records * tf.repeats))
+                assert b.tobytes() == eb, ("pair chunk bytes differ", j, f)
+                nl = np.nonzero(np.frombuffer(eb, np.uint8) == 10)[0].astype(np.uint32).reshape(-1, 4)
+                assert np.array_equal(d, nl), ("pair chunk descriptors differ", j, f)
+                want.add(j)
+    return f"{len(want)} pair chunks of rank {rank} byte-compared with the members' text" if want else "none on this rank"
+
+
+_REC_STARTS = {}
+
+
+def tiled_records(tf, lo, hi):
+    """Bytes of records [lo, hi) of a tiled member (its segment's records repeated)."""
+    key = id(tf.text)
+    if key not in _REC_STARTS:
+        nl = np.nonzero(np.asarray(tf.text) == 10)[0]
+        _REC_STARTS[key] = np.concatenate([[0], nl[3::4] + 1]).astype(np.int64)
+    st = _REC_STARTS[key]
+    n = tf.records
+    out = []
+    i = lo
+    while i < hi:
+        r = i % n
+        take = min(hi - i, n - r)
+        out.append(np.asarray(tf.text[int(st[r]):int(st[r + take])]).tobytes())
+        i += take
+    return b"".join(out)
 
 
 def wave_slots(dev):
@@ -777,6 +868,10 @@ def main():
     ap.add_argument("--paired", action="store_true",
                     help="configs[4]-shaped paired-end run on one GPU (prints its own line instead)")
     ap.add_argument("--paired-repeats", type=int, default=0)   # 0: 102 (configs[4]: ~25 GB gz per file)
+    ap.add_argument("--pair-chunk", type=int, default=50_000,
+                    help="--paired: pairs per record-aligned pair chunk (BASELINE configs[4]: 50,000)")
+    ap.add_argument("--pair-window-gib", type=float, default=8.0,
+                    help="--paired: device bytes per emission window and file (ppg_pairs_emit_begin)")
     ap.add_argument("--paired-out-gib", type=float, default=56.0,
                     help="--paired: output buffer per file in GiB (a rank's range decodes in batches of this; the "
                          "spot keys are extracted per batch)")

@@ -145,10 +145,12 @@ int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream);
  * (LazyFileReader.cs:63-69).  out receives to.Output-from.Output bytes; `produced` the count
  * (Core.cs:191).  If recs is non-NULL, up to rec_cap records are written as 4 uint32 newline
  * positions (n1..n4) relative to raw = offset_k ++ out; *nrec gets the record count.
- * Thread safe (README.md:38-50): concurrent calls on one ctx are combined into shared launches (two
+ * Thread safe (README.md:38-50): concurrent calls on one ctx are combined into shared launches (four
  * launch slots, each with its own stream and buffers that only grow: no hipMalloc/hipFree per call
- * once warm); every call gets its own chunk's results.  A chunk of an index with side points
- * (ppg_index_build_gpu_side) is decoded as one wave per piece; in a launch of at most 256 chunks,
+ * once warm; a second launch starts beside a decoding one only once 16 calls queue, so the queue
+ * that builds up during a launch goes into the next one); every call gets its own chunk's results.
+ * A chunk of an index with side points
+ * (ppg_index_build_gpu_side) is decoded as one wave per piece; in a launch of at most 4,096 chunks,
  * a chunk of an index without them gets its inner block starts found on the GPU first (candidate
  * block headers, a speculative symbolic decode, the verified chain of block ends from the chunk's
  * Point and their resolved 32 KiB histories -- CreateIndex's own kernels) and is decoded as up to
@@ -156,8 +158,19 @@ int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream);
 int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
                          uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
                          int64_t *nrec);
-/* ppg_decompress_chunk calls on this ctx so far, the launches that served them, the most calls one
- * launch served. */
+/* The same, asynchronous: one caller keeps many chunks in flight, as the reference's reader keeps 32
+ * partitions queued (LazyFileReader.cs:14) for its tasks.  submit queues the request and returns a
+ * ticket at once; a launcher thread of the ctx (started by the first submit) combines the queued
+ * requests -- a burst of submissions goes into one launch of up to 1,024 chunks -- and
+ * ppg_decompress_chunk_wait blocks until the ticket's chunk is decoded, copies its bytes / records
+ * into the buffers given at submit (slice, out and recs must stay valid until then) and frees the
+ * ticket.  Every ticket must be waited for, each once, on the ctx it was submitted to. */
+typedef struct ppg_chunk_req ppg_chunk_req;
+int ppg_decompress_chunk_submit(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
+                                uint8_t *out, int64_t out_cap, uint32_t *recs, int64_t rec_cap, ppg_chunk_req **req);
+int ppg_decompress_chunk_wait(ppg_ctx *ctx, ppg_chunk_req *req, int64_t *produced, int64_t *nrec);
+/* ppg_decompress_chunk (and _submit) calls on this ctx so far, the launches that served them, the
+ * most calls one launch served. */
 int ppg_decompress_chunk_stats(ppg_ctx *ctx, int64_t *calls, int64_t *launches, int64_t *max_batch);
 /* Chunks split by the search for inner block starts above, and the side points it found. */
 int ppg_decompress_chunk_split_stats(ppg_ctx *ctx, int64_t *chunks, int64_t *side_points);
@@ -354,6 +367,39 @@ int ppg_pairs_check(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *comm, 
  * numbers [j*K, (j+1)*K); the records themselves via ppg_shard_record_base / ppg_shard_copy_records. */
 int ppg_pairs_records(const ppg_pairs *p, int32_t file, int64_t lo, int64_t hi, int64_t *shard_record);
 void ppg_pairs_free(ppg_pairs *p);
+
+/* ---- record-aligned pair chunks (BASELINE configs[4]: "chunk=50 000, record-aligned
+ * pair chunks"; the reference's goal, README.md:9) ----
+ * After ppg_pairs_check: pair chunk j = pairs [j*K, min((j+1)*K, pairs)).  Each half (file 0 = R1,
+ * 1 = R2) is packed contiguously on the device: its records' bytes back to back -- each record from
+ * its '@' to its quality line's '\n', the FastqRecord copy of Parsing.cs:41-47 -- and one 16-B
+ * descriptor (n1, n2, n3, n4: the record's newline positions) per record, relative to the half's
+ * first byte: the layout of one chunk's raw text + descriptors, so the same record reader applies
+ * (record i starts at n4[i-1] + 1, record 0 at 0).
+ *  ppg_pairs_emit_begin  the plan for this rank's pair chunks, on the shards and comm of the check.
+ *      One rank: every pair chunk, in windows of at most window_bytes per half-file (0: 8 GiB; one
+ *      pair chunk at least).  Multi-batch shards (configs[4]'s 2 x 25 GB on one GPU) have their
+ *      batches run again as the windows advance -- both files' together, each on its own stream --
+ *      and a pair chunk that straddles a batch boundary is carried across; nothing else may run the
+ *      shards until the emission is done.  N ranks: rank r owns the pair chunks that start in its
+ *      R1 range; the shards must be one-batch (resident; else PPG_UNSUPPORTED).
+ *  ppg_pairs_emit_next   packs the next window of this rank's pair chunks [*j0, *j1) on the device;
+ *      PPG_STREAM_END when there is none.  N ranks: the first call is collective (every rank calls
+ *      it: the records a rank does not hold move from their ranks over ppg_comm_alltoallv -- RCCL
+ *      ncclSend / ncclRecv over xGMI, or the host transport) and is the rank's one window.
+ *  ppg_pairs_chunk       device pointers of a half of the current window (valid until the next call).
+ *  ppg_pairs_copy_chunk  a half into caller memory (bytes and/or descriptors; NULL skips).
+ *  ppg_pairs_emit_stats  [0] ms re-running batches, [1] ms packing, [2] ms exchanging, [3] ms in
+ *      emit_next, [4] batches re-run, [5] pair chunks in all, [6..7] this rank's [j_lo, j_hi)
+ *      (N ranks: after the exchange). */
+int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *comm, int64_t pair_chunk,
+                         int64_t window_bytes);
+int ppg_pairs_emit_next(ppg_pairs *p, int64_t *j0, int64_t *j1);
+int ppg_pairs_chunk(ppg_pairs *p, int64_t j, int32_t file, const uint8_t **bytes, int64_t *len, const uint32_t **desc,
+                    int64_t *nrec);
+int ppg_pairs_copy_chunk(ppg_pairs *p, int64_t j, int32_t file, uint8_t *dst, int64_t cap, int64_t *len, uint32_t *desc,
+                         int64_t desc_cap, int64_t *nrec);
+int ppg_pairs_emit_stats(const ppg_pairs *p, double *vals, int32_t n);
 
 /* Library build string (kernel ISA, version). */
 const char *ppg_version(void);

@@ -5,10 +5,13 @@
 //    and paired on the device by ppg_pairs_check: spot keys, the records the reference parses twice
 //    dropped (SURVEY Q1), keys compared -- a file pair that is not a read pair throws before any pair
 //    is handed out;
-//  * pair chunk j = pairs [j*K, (j+1)*K): ppg_pairs_records maps pair numbers to each shard's record
-//    numbers, whose FastqRecords are cut from raw_k = offset_k ++ chunk_k as Parsing.cs:23-47 cuts them;
+//  * pair chunk j = pairs [j*K, (j+1)*K): the library packs both halves on the device window by
+//    window (ppg_pairs_emit_begin / _next: each half is its records' bytes back to back + one
+//    descriptor per record, the layout of one chunk's raw text), and each half crosses to the host
+//    in one copy (ppg_pairs_copy_chunk), whose FastqRecords are cut as Parsing.cs:23-47 cuts them;
 //  * a multi-GPU job (GpuJob) checks its ranks' shards together (CheckDistributed): every key moves to
-//    the rank owning its pair number over the library's RCCL communicator.
+//    the rank owning its pair number over the library's RCCL communicator; EmitDistributed then hands
+//    each rank the pair chunks that start in its R1 range, the mates' records moved to it over RCCL.
 // (Source only: no .NET SDK in this image; tests/test_interop_cs.py checks the externs it uses.)
 using System;
 using System.Collections;
@@ -85,67 +88,63 @@ public sealed unsafe class GpuPairedFASTQ : IEnumerable<(FastqRecord R1, FastqRe
         return f;
     }
 
-    /// <summary>(R1 records, R2 records) of pair chunk j: pairs [j*K, min((j+1)*K, Count)).</summary>
-    public (FastqRecord[] R1, FastqRecord[] R2) PairChunk(long j)
+    /// <summary>Every pair chunk in order: (j, R1 records, R2 records), pairs [j*K, min((j+1)*K, Count)),
+    /// from the library's device-packed windows (ppg_pairs_emit_next).</summary>
+    public IEnumerable<(long J, FastqRecord[] R1, FastqRecord[] R2)> PairChunks(long windowBytes = 0)
     {
-        long lo = j * _K, hi = Math.Min(lo + _K, _Result.Pairs);
-        if (j < 0 || lo >= hi) throw new ArgumentOutOfRangeException(nameof(j));
-        return (Records(0, lo, hi), Records(1, lo, hi));
+        PpGpu.Check(PpGpu.ppg_pairs_emit_begin(_Pairs, _Files[0].Shard, _Files[1].Shard, 0, _K, windowBytes));
+        for (;;)
+        {
+            int rc = PpGpu.ppg_pairs_emit_next(_Pairs, out long j0, out long j1);
+            if (rc == 1) yield break;   // PPG_STREAM_END
+            PpGpu.Check(rc);
+            for (long j = j0; j < j1; j++) yield return (j, Half(_Pairs, j, 0), Half(_Pairs, j, 1));
+        }
     }
 
-    private FastqRecord[] Records(int file, long lo, long hi)
+    /// <summary>A multi-GPU job's pair chunks on this rank (after CheckDistributed on the same shards):
+    /// the ones that start in its R1 range; every rank must call it (the first window is collective).</summary>
+    public static IEnumerable<(long J, FastqRecord[] R1, FastqRecord[] R2)> EmitDistributed(GpuJob job, nint pairs,
+        nint shardR1, nint shardR2, int pairChunk)
     {
-        var f = _Files[file];
-        var rec = new long[hi - lo];
-        fixed (long* r = rec) PpGpu.Check(PpGpu.ppg_pairs_records(_Pairs, file, lo, hi, r));
-        var outp = new FastqRecord[rec.Length];
-        int cached = -1;
-        byte[] raw = Array.Empty<byte>();
-        uint[] desc = Array.Empty<uint>();
-        for (long i = 0; i < rec.Length; i++)
+        PpGpu.Check(PpGpu.ppg_pairs_emit_begin(pairs, shardR1, shardR2, job.Comm, pairChunk, 0));
+        for (;;)
         {
-            int k = Array.BinarySearch(f.Bases, rec[i]);
-            if (k < 0) k = ~k - 1;
-            while (k + 1 < f.Bases.Length && f.Bases[k + 1] <= rec[i]) k++;   // chunks without records
-            if (k != cached)
-            {
-                (raw, desc) = Chunk(f, k);
-                cached = k;
-            }
-            long j = rec[i] - f.Bases[k];
-            uint start = j == 0 ? 0u : desc[4 * j - 1] + 1;   // Parsing.cs:19: raw[start] is the '@'
-            var m = new Memory<byte>(raw);
+            int rc = PpGpu.ppg_pairs_emit_next(pairs, out long j0, out long j1);
+            if (rc == 1) yield break;
+            PpGpu.Check(rc);
+            for (long j = j0; j < j1; j++) yield return (j, Half(pairs, j, 0), Half(pairs, j, 1));
+        }
+    }
+
+    // one half: its bytes and descriptors in one copy each, FastqRecords over them
+    private static FastqRecord[] Half(nint pairs, long j, int file)
+    {
+        PpGpu.Check(PpGpu.ppg_pairs_chunk(pairs, j, file, out _, out long len, out _, out long n));
+        var raw = new byte[len];
+        var desc = new uint[4 * n];
+        fixed (byte* b = raw)
+        fixed (uint* d = desc)
+            PpGpu.Check(PpGpu.ppg_pairs_copy_chunk(pairs, j, file, b, len, out _, d, n, out _));
+        var outp = new FastqRecord[n];
+        var m = new Memory<byte>(raw);
+        uint start = 0;   // Parsing.cs:19: raw[start] is the '@'
+        for (long i = 0; i < n; i++)
+        {
             outp[i] = new FastqRecord(null!,
-                m.Slice((int)start + 1, (int)(desc[4 * j] - start - 1)),
-                m.Slice((int)desc[4 * j] + 1, (int)(desc[4 * j + 1] - desc[4 * j] - 1)),
-                m.Slice((int)desc[4 * j + 1] + 2, (int)(desc[4 * j + 2] - desc[4 * j + 1] - 2)),
-                m.Slice((int)desc[4 * j + 2] + 1, (int)(desc[4 * j + 3] - desc[4 * j + 2] - 1)));
+                m.Slice((int)start + 1, (int)(desc[4 * i] - start - 1)),
+                m.Slice((int)desc[4 * i] + 1, (int)(desc[4 * i + 1] - desc[4 * i] - 1)),
+                m.Slice((int)desc[4 * i + 1] + 2, (int)(desc[4 * i + 2] - desc[4 * i + 1] - 2)),
+                m.Slice((int)desc[4 * i + 2] + 1, (int)(desc[4 * i + 3] - desc[4 * i + 2] - 1)));
+            start = desc[4 * i + 3] + 1;
         }
         return outp;
     }
 
-    // raw_k = offset_k ++ chunk_k and chunk k's descriptors
-    private static (byte[] raw, uint[] desc) Chunk(File1 f, int k)
-    {
-        PpGpu.Check(PpGpu.ppg_index_point(f.Index, k, out long o0, out _, out _, out int olen));
-        PpGpu.Check(PpGpu.ppg_index_point(f.Index, k + 1, out long o1, out _, out _, out _));
-        var raw = new byte[olen + (o1 - o0)];
-        new ReadOnlySpan<byte>(PpGpu.ppg_index_offset(f.Index, k), olen).CopyTo(raw);
-        fixed (byte* p = raw)
-            PpGpu.Check(PpGpu.ppg_shard_copy_chunk(f.Shard, k, p + olen, o1 - o0, out _));
-        PpGpu.Check(PpGpu.ppg_shard_copy_records(f.Shard, k, null, 0, out long n));
-        var desc = new uint[4 * n];
-        fixed (uint* d = desc) PpGpu.Check(PpGpu.ppg_shard_copy_records(f.Shard, k, d, n, out _));
-        return (raw, desc);
-    }
-
     public IEnumerator<(FastqRecord R1, FastqRecord R2)> GetEnumerator()
     {
-        for (long j = 0; j < Chunks; j++)
-        {
-            var (a, b) = PairChunk(j);
+        foreach (var (_, a, b) in PairChunks())
             for (int i = 0; i < a.Length; i++) yield return (a[i], b[i]);
-        }
     }
 
     IEnumerator IEnumerable.GetEnumerator() => GetEnumerator();

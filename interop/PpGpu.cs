@@ -97,6 +97,11 @@ internal static unsafe class PpGpu
     // ---- README "Decompress": Core.ExtractDeflateIndex (Core.cs:133-192) + Parsing.Parse ----
     [DllImport(Lib)] public static extern int ppg_decompress_chunk(nint ctx, nint ix, int k, byte* slice,
         long sliceLen, byte* output, long outCap, out long produced, uint* recs, long recCap, out long nrec);
+    // asynchronous Decompress: many chunks in flight from one caller (ppg_decompress_chunk_submit / _wait)
+    [DllImport(Lib)] public static extern int ppg_decompress_chunk_submit(nint ctx, nint ix, int k, byte* slice,
+        long sliceLen, byte* outp, long outCap, uint* recs, long recCap, out nint req);
+    [DllImport(Lib)] public static extern int ppg_decompress_chunk_wait(nint ctx, nint req, out long produced,
+        out long nrec);
     [DllImport(Lib)] public static extern int ppg_decompress_chunk_stats(nint ctx, out long calls, out long launches,
         out long maxBatch);
     [DllImport(Lib)] public static extern int ppg_decompress_chunk_split_stats(nint ctx, out long chunks,
@@ -161,6 +166,15 @@ internal static unsafe class PpGpu
     [DllImport(Lib)] public static extern int ppg_pairs_records(nint pairs, int file, long lo, long hi,
         long* shardRecord);
     [DllImport(Lib)] public static extern void ppg_pairs_free(nint pairs);
+    // record-aligned pair chunks, packed on the device (ppg_pairs_emit_*)
+    [DllImport(Lib)] public static extern int ppg_pairs_emit_begin(nint pairs, nint r1, nint r2, nint comm,
+        long pairChunk, long windowBytes);
+    [DllImport(Lib)] public static extern int ppg_pairs_emit_next(nint pairs, out long j0, out long j1);
+    [DllImport(Lib)] public static extern int ppg_pairs_chunk(nint pairs, long j, int file, out nint bytes, out long len,
+        out nint desc, out long nrec);
+    [DllImport(Lib)] public static extern int ppg_pairs_copy_chunk(nint pairs, long j, int file, byte* dst, long cap,
+        out long len, uint* desc, long descCap, out long nrec);
+    [DllImport(Lib)] public static extern int ppg_pairs_emit_stats(nint pairs, double* vals, int n);
 
     [DllImport(Lib)] public static extern nint ppg_version();
     [DllImport(Lib)] public static extern nint ppg_build_id();

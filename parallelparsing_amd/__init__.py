@@ -375,6 +375,51 @@ class Core:
             return produced.value, buf, recs[:nrec.value]
         return produced.value, buf
 
+    @staticmethod
+    def ExtractDeflateIndexAsync(file_buffer, index, k, buf=None, device=None):
+        """ExtractDeflateIndex queued without blocking (ppg_decompress_chunk_submit): returns a
+        ChunkFuture whose result() is (produced, buf, records).  Many queued chunks share launches
+        of up to 1,024 chunks; every future's result() must be taken (it frees the ticket)."""
+        dev = device or Device.default()
+        src = _as_u8(file_buffer)
+        o0, _, _, _ = index.point_fields(k)
+        o1, _, _, _ = index.point_fields(k + 1)
+        need = max(0, o1 - o0)
+        if buf is None:
+            buf = np.empty(need, np.uint8)
+        recs = np.empty((max(1, need // 4 + 1), 4), np.uint32)
+        t = C.c_void_p()
+        check(lib.ppg_decompress_chunk_submit(dev.handle, index.handle, int(k), _ptr(src), src.size, _ptr(buf), buf.size,
+                                              _ptr(recs), recs.shape[0], C.byref(t)), "ppg_decompress_chunk_submit")
+        return ChunkFuture(dev, t, (src, buf, recs, index))
+
+
+class ChunkFuture:
+    """A queued ExtractDeflateIndexAsync: result() waits (ppg_decompress_chunk_wait) -- once."""
+
+    def __init__(self, dev, ticket, keep):
+        self._dev, self._t, self._keep, self._res = dev, ticket, keep, None
+
+    def result(self):
+        if self._res is None:
+            produced, nrec = C.c_int64(), C.c_int64()
+            t, self._t = self._t, None
+            if t is None:
+                raise RuntimeError("ChunkFuture waited twice")
+            rc = lib.ppg_decompress_chunk_wait(self._dev.handle, t, C.byref(produced), C.byref(nrec))
+            _, buf, recs, _ = self._keep
+            self._keep = None
+            check(rc, "Core.ExtractDeflateIndexAsync")
+            self._res = (produced.value, buf, recs[:nrec.value])
+        return self._res
+
+    def __del__(self):
+        if getattr(self, "_t", None) is not None:   # never waited: wait now (the buffers must outlive it)
+            try:
+                self.result()
+            except Exception:   # noqa: BLE001 - a finaliser must not raise
+                pass
+
 
 class Shard:
     """DecompressAll over index chunks [first, first+n) resident on one GPU (ppg_shard)."""

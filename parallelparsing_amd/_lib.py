@@ -91,6 +91,8 @@ _SIGS = {
     "ppg_stream_wait_ctx": (C.c_int, [vp, vp]),
     "ppg_decompress_chunk": (C.c_int, [vp, vp, i32, vp, i64, vp, i64, P(i64), vp, i64, P(i64)]),
     "ppg_decompress_chunk_stats": (C.c_int, [vp, P(i64), P(i64), P(i64)]),
+    "ppg_decompress_chunk_submit": (C.c_int, [vp, vp, i32, vp, i64, vp, i64, vp, i64, P(vp)]),
+    "ppg_decompress_chunk_wait": (C.c_int, [vp, vp, P(i64), P(i64)]),
     "ppg_decompress_chunk_split_stats": (C.c_int, [vp, P(i64), P(i64)]),
     "ppg_shard_create": (C.c_int, [vp, vp, i32, i32, vp, i64, C.c_int, i64, P(vp)]),
     "ppg_shard_free": (None, [vp]),
@@ -130,6 +132,11 @@ _SIGS = {
     "ppg_pairs_check": (C.c_int, [vp, vp, vp, vp, vp]),
     "ppg_pairs_records": (C.c_int, [vp, i32, i64, i64, vp]),
     "ppg_pairs_free": (None, [vp]),
+    "ppg_pairs_emit_begin": (C.c_int, [vp, vp, vp, vp, i64, i64]),
+    "ppg_pairs_emit_next": (C.c_int, [vp, P(i64), P(i64)]),
+    "ppg_pairs_chunk": (C.c_int, [vp, i64, i32, P(vp), P(i64), P(vp), P(i64)]),
+    "ppg_pairs_copy_chunk": (C.c_int, [vp, i64, i32, vp, i64, P(i64), vp, i64, P(i64)]),
+    "ppg_pairs_emit_stats": (C.c_int, [vp, P(C.c_double), i32]),
 }
 
 

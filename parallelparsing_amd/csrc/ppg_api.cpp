@@ -40,8 +40,8 @@ hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgIn
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n, const uint32_t *nls);
 hipError_t ppg_launch_split_merge(hipStream_t s, const PpgInflateJob *sjobs, const PpgInflateResult *sres,
-                                  const uint32_t *sidx, const uint32_t *snls, const PpgInflateJob *jobs,
-                                  PpgInflateResult *res, uint32_t *nls, int n);
+                                  const uint32_t *inv, const uint32_t *sidx, const uint32_t *snls,
+                                  const PpgInflateJob *jobs, PpgInflateResult *res, uint32_t *nls, int n);
 hipError_t ppg_launch_parse_emit(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                  const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                  PpgParseInfo *info, const uint64_t *base, const uint32_t *nls, uint32_t *recs,
@@ -606,6 +606,8 @@ int shard_reserve(ppg_shard *sh, const ppg_index *ix, int32_t first,
     HIPCHK(sh->nls.alloc((size_t)nl_max + 64));
     if (nsub_max) {
         HIPCHK(sh->sjobs.alloc((size_t)(n_max + nsub_max)));
+        HIPCHK(sh->ljobs.alloc((size_t)(n_max + nsub_max)));
+        HIPCHK(sh->linv.alloc((size_t)(n_max + nsub_max)));
         HIPCHK(sh->sres.alloc((size_t)(n_max + nsub_max)));
         HIPCHK(sh->sidx.alloc((size_t)n_max + 1));
     }
@@ -653,13 +655,14 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     hipStream_t s = shard_stream(sh);
     const int nb = b1 - b0;
     HIPCHK(hipEventRecord(sh->ev[0], s));
-    if (sh->nsub) {   // the batch's sub-jobs, then one result per chunk
+    if (sh->nsub) {   // the batch's sub-jobs (longest first, see ppg_shard_set_split), then one result per chunk
         const uint32_t s0 = sh->h_sidx[(size_t)b0], s1 = sh->h_sidx[(size_t)b1];
+        const bool lpt = sh->lpt;
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
-                                  sh->sjobs.p + s0, sh->dicts.p, sh->out.p, sh->sres.p + s0, (int)(s1 - s0),
-                                  sh->nls.p));
-        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->sidx.p + b0, sh->nls.p, sh->jobs.p + b0,
-                                      sh->res.p + b0, sh->nls.p, nb));
+                                  (lpt ? sh->ljobs.p : sh->sjobs.p) + s0, sh->dicts.p, sh->out.p, sh->sres.p + s0,
+                                  (int)(s1 - s0), sh->nls.p));
+        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, lpt ? sh->linv.p : nullptr, sh->sidx.p + b0, sh->nls.p,
+                                      sh->jobs.p + b0, sh->res.p + b0, sh->nls.p, nb));
     } else {
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
                                   sh->jobs.p + b0, sh->dicts.p, sh->out.p, sh->res.p + b0, nb, sh->nls.p));
@@ -870,6 +873,34 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
         HIPCHK(sh->nls.alloc((size_t)nl_need + 64));
     }
     sh->h_sidx = hidx;
+    // launch order: within each batch the sub-jobs longest first (LPT), so the launch drains on its
+    // shortest pieces -- a chunk's pieces are whole deflate blocks of similar size, but the last one
+    // before a Point, a pigz piece's flush block and a chunk left whole are not.  The results land
+    // in launch order and ppg_split_merge reads them through the inverse permutation.
+    // PPG_SPLIT_ORDER=0: the sub-jobs in chunk order.
+    static const bool lpt_off = [] { const char *e = getenv("PPG_SPLIT_ORDER"); return e && *e == '0'; }();
+    sh->lpt = !lpt_off;
+    if (sh->lpt) {
+        const size_t ns = sh->h_sjobs.size();
+        std::vector<uint32_t> perm(ns), inv(ns);
+        std::vector<PpgInflateJob> lj(ns);
+        for (auto [b0, b1] : sh->batches) {
+            const uint32_t s0 = hidx[(size_t)b0], s1 = hidx[(size_t)b1];
+            for (uint32_t j = s0; j < s1; j++) perm[j] = j;
+            std::stable_sort(perm.begin() + s0, perm.begin() + s1, [&](uint32_t a, uint32_t b) {
+                return sh->h_sjobs[a].out_len > sh->h_sjobs[b].out_len;
+            });
+        }
+        for (size_t q = 0; q < ns; q++) {
+            lj[q] = sh->h_sjobs[perm[q]];
+            inv[perm[q]] = (uint32_t)q;
+        }
+        HIPCHK(sh->ljobs.alloc(ns));
+        HIPCHK(sh->linv.alloc(ns));
+        HIPCHK(hipMemcpyAsync(sh->ljobs.p, lj.data(), sizeof(PpgInflateJob) * ns, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(sh->linv.p, inv.data(), 4 * ns, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     HIPCHK(hipStreamSynchronize(s));   // staging vectors and d2 (the old dictionaries) die here
     sh->nsub = nsub;
     return PPG_OK;

@@ -19,9 +19,11 @@
 // piece between their inner block starts (ppg_shard_set_split), exactly as DecompressAll does.
 #include "ppg_host.h"
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <thread>
 
 hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
                                  const uint64_t *hi, uint64_t *cand, int n);
@@ -36,16 +38,29 @@ int ppg_resolve_groups(int np);
 
 namespace {
 
-constexpr int kChunkSlots = 2;
+constexpr int kChunkSlots = 4;             // launches in flight / results being copied out
 constexpr uint64_t kPieceRing = 65536;     // CreateIndex pass 1's symbolic output ring per piece (IX_RING_BYTES)
-constexpr int kFindMaxChunks = 256;        // launches of more chunks fill the GPU by themselves
+// launches of up to this many chunks split them at their inner block starts found on the GPU: ~16
+// waves per chunk, so 4,096 chunks already hold ~8 generations of the GPU's 8,192 wave slots
+constexpr int kFindMaxChunks = 4096;
 constexpr size_t kSliceAlign = 64;   // each gathered slice starts on its own 64-B line
+constexpr size_t kMaxBatch = 1024;         // chunks per launch
+// a second launch starts while one is decoding only with this many requests queued: otherwise the
+// queue grows during the running launch and the next one takes all of it (r04: with two slots taken
+// as soon as free, 64 callers were served ~12 at a time)
+constexpr size_t kMinSecond = 16;
 
 struct ChunkReq {
     const ppg_index *ix;
     int32_t k;
     const uint8_t *slice;
     int64_t slice_len;
+    // asynchronous requests (ppg_decompress_chunk_submit): where wait() copies the results
+    bool async = false;
+    uint8_t *out = nullptr;
+    int64_t out_cap = 0;
+    uint32_t *recs = nullptr;
+    int64_t rec_cap = 0;
     // results, set by the launching caller
     bool done = false;
     int rc = PPG_OK;
@@ -94,13 +109,25 @@ struct ChunkService {
     std::deque<ChunkReq *> pending;
     ChunkSlot slot[kChunkSlots];
     int64_t calls = 0, launches = 0, max_batch = 0;
+    int in_flight = 0;                                         // launches decoding now
     std::atomic<int64_t> found_chunks{0}, found_points{0};   // find_side_points' splits
+    // the launcher of asynchronous requests (started by the first ppg_decompress_chunk_submit)
+    ppg_ctx *ctx = nullptr;
+    std::thread worker;
+    bool stop = false;
+    std::chrono::steady_clock::time_point last_submit{};
 };
 
 ChunkService *chunk_service_new() { return new ChunkService; }
 
 void chunk_service_free(ChunkService *svc) {
     if (!svc) return;
+    {
+        std::lock_guard<std::mutex> lk(svc->mu);
+        svc->stop = true;
+    }
+    svc->cv.notify_all();
+    if (svc->worker.joinable()) svc->worker.join();
     for (auto &sl : svc->slot) {
         if (sl.sh) ppg_shard_free(sl.sh);
         if (sl.s) (void)hipStreamDestroy(sl.s);
@@ -147,6 +174,28 @@ bool side_points_inside(const ppg_index *ix, int32_t k) {
     return true;
 }
 
+// PPG_CHUNK_VERBOSE=1: a launch's phases (ms) on stderr -- where a lone chunk's latency goes
+struct PhaseClock {
+    bool on;
+    std::chrono::steady_clock::time_point t0, t;
+    char buf[512];
+    int n = 0;
+    PhaseClock() : on(getenv("PPG_CHUNK_VERBOSE") != nullptr) { t0 = t = std::chrono::steady_clock::now(); buf[0] = 0; }
+    void mark(const char *what, hipStream_t s = nullptr) {
+        if (!on) return;
+        if (s) (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        n += snprintf(buf + n, sizeof buf - (size_t)n, " %s %.3f", what,
+                      std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+        if (n >= (int)sizeof buf) n = (int)sizeof buf - 1;
+    }
+    void dump(size_t reqs) {
+        if (on) fprintf(stderr, "PPG_CHUNK launch of %zu: total %.3f ms:%s\n", reqs,
+                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), buf);
+    }
+};
+
 // Side points for chunks whose index has none (a .gzi carries only the Points): the inner deflate
 // block starts of each chunk found on the GPU the way the GPU CreateIndex finds them
 // (ppg_index_gpu.cpp) -- candidate dynamic-block headers every ~1/16 of the chunk's compressed bytes
@@ -167,7 +216,8 @@ struct FindChunk {
 };
 
 int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const std::vector<FindChunk> &ch,
-                     std::vector<int64_t> &sbit, std::vector<int64_t> &sout, ByteVec &swin, int64_t &nsplit) {
+                     std::vector<int64_t> &sbit, std::vector<int64_t> &sout, ByteVec &swin, int64_t &nsplit,
+                     PhaseClock &clk) {
     hipStream_t s = sl.s;
     FindScratch &F = sl.fs;
     // candidates: the chunk cut into up to 16 pieces of >= 48 KiB of compressed bytes
@@ -193,6 +243,7 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
     std::vector<uint64_t> cand(nc);
     HIPCHK(hipMemcpyAsync(cand.data(), F.cand.p, 8 * nc, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    clk.mark("f.cand");
     // pieces: chunk c's Point, then its candidates; every piece but the last decoded to the next
     struct Piece { size_t chunk; uint64_t start, stop; };
     std::vector<Piece> pc;
@@ -240,6 +291,7 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
     // the symbolic tails: the last 32 Ki symbols of each piece's ring, as two 32 KiB byte halves
     std::vector<PpgGather> g(2 * np);
     HIPCHK(hipStreamSynchronize(s));
+    clk.mark("f.pass1");
     for (size_t q = 0; q < np; q++) {
         const uint64_t endb = 2 * res[q].produced;
         g[2 * q] = PpgGather{(uint64_t)q * 2 * kPieceRing, (uint64_t)kWin, endb - kWin, 2 * kPieceRing - 1, 0};
@@ -319,6 +371,7 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
         nsplit += any;
     }
     HIPCHK(hipStreamSynchronize(s));
+    clk.mark("f.resolve");
     return PPG_OK;
 }
 
@@ -326,6 +379,7 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
 // every request's rc and, for a decoded chunk, where its bytes and descriptors sit in sl.res.
 int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<ChunkReq *> &batch) {
     HIPCHK(hipSetDevice(ctx->device));
+    PhaseClock pc;
     if (!sl.s) HIPCHK(hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking));
     if (!sl.sh) {
         sl.sh = new ppg_shard;
@@ -389,8 +443,10 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     for (size_t i = 0; i < go.size(); i++) memcpy(sl.in.p + at[i], go[i]->slice, (size_t)go[i]->slice_len);
     HIPCHK(hipMemcpyAsync(sl.comp.p, sl.in.p, comp_len + 256, hipMemcpyHostToDevice, sl.s));
     ppg_shard *sh = sl.sh;
+    pc.mark("h2d", sl.s);
     int rc = shard_prepare_specs(sh, spec.data(), (int32_t)go.size(), sl.comp.p, (int64_t)comp_len, 0, sl.s, nullptr);
     if (rc != PPG_OK) return rc;
+    pc.mark("prepare");
     {   // side points of the chunks that have them (the index's, shifted into this launch); the
         // others' found on the GPU when the launch is too small to fill it
         std::vector<int64_t> sbit, sout;
@@ -409,22 +465,25 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
             if (!find.empty() && (i + 1 == go.size() || !go[i + 1]->ix->side_out.empty())) {
                 const size_t before = sbit.size();
                 int64_t nsplit = 0;
-                rc = find_side_points(sl, (const uint32_t *)sl.comp.p, sh->nwords, find, sbit, sout, swin, nsplit);
+                rc = find_side_points(sl, (const uint32_t *)sl.comp.p, sh->nwords, find, sbit, sout, swin, nsplit, pc);
                 if (rc != PPG_OK) return rc;
                 svc.found_chunks += nsplit;
                 svc.found_points += (int64_t)(sbit.size() - before);
                 find.clear();
             }
         }
+        pc.mark("find");
         if (!sbit.empty()) {
             rc = ppg_shard_set_split(sh, (int32_t)sbit.size(), sbit.data(), sout.data(), swin.data());
             if (rc != PPG_OK) return rc;
         }
+        pc.mark("split");
     }
     shard_reset(sh);
     float total_ms = 0;
     if ((rc = batch_launch(sh, 0, sh->n)) != PPG_OK) return rc;
     if ((rc = batch_collect(sh, 0, sh->n, total_ms)) != PPG_OK) return rc;
+    pc.mark("decode");
     // shard_finish returns the first chunk's zlib status (each request gets its own below) or a
     // device failure, which fails every request of the launch
     if ((rc = shard_finish(sh, total_ms)) <= PPG_INDEX_OUT_OF_RANGE) return rc;
@@ -436,6 +495,8 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     if (out_bytes) HIPCHK(hipMemcpyAsync(sl.res.p, sh->out.p, out_bytes, hipMemcpyDeviceToHost, sl.s));
     if (rec_bytes) HIPCHK(hipMemcpyAsync(sl.res.p + rec_at, sh->recs.p, rec_bytes, hipMemcpyDeviceToHost, sl.s));
     HIPCHK(hipStreamSynchronize(sl.s));
+    pc.mark("d2h");
+    pc.dump(go.size());
     for (size_t i = 0; i < go.size(); i++) {
         ChunkReq *r = go[i];
         const PpgInflateResult &res = sh->h_res[i];
@@ -450,57 +511,58 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-// README "Decompress" (see the top of this file).  Safe to call from any number of host threads
-// on one ctx at once.
-int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
-                         uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
-                         int64_t *nrec) {
-    if (!ctx || !ix || !slice || k < 0 || (size_t)k + 1 >= ix->pts.size() || !ctx->chunks) return PPG_ARG_ERROR;
-    ChunkService *svc = ctx->chunks;
-    ChunkReq req{ix, k, slice, slice_len};
-    std::unique_lock<std::mutex> lk(svc->mu);
-    svc->calls++;
-    svc->pending.push_back(&req);
-    while (!req.done) {
-        int free_slot = -1;
-        for (int i = 0; i < kChunkSlots && free_slot < 0; i++)
-            if (!svc->slot[i].busy && svc->slot[i].readers == 0) free_slot = i;
-        if (free_slot < 0 || svc->pending.empty()) {
-            svc->cv.wait(lk);
-            continue;
-        }
-        // lead a launch of every queued request (this one among them, unless another caller took it)
-        std::vector<ChunkReq *> batch(svc->pending.begin(), svc->pending.end());
-        svc->pending.clear();
-        ChunkSlot &sl = svc->slot[free_slot];
-        sl.busy = true;
-        svc->launches++;
-        svc->max_batch = std::max<int64_t>(svc->max_batch, (int64_t)batch.size());
-        lk.unlock();
-        int rc;
-        try {
-            rc = run_launch(ctx, *svc, sl, batch);
-        } catch (const std::bad_alloc &) {   // host vectors: never out through the C ABI, never a stuck slot
-            rc = PPG_MEM_ERROR;
-        } catch (...) {
-            rc = PPG_DEVICE_ERROR;
-        }
-        lk.lock();
-        for (ChunkReq *r : batch) {
-            if (rc != PPG_OK) r->rc = rc;
-            if (r->rc == PPG_OK) {
-                r->slot = free_slot;
-                sl.readers++;
-            }
-            r->done = true;
-        }
-        sl.busy = false;
-        svc->cv.notify_all();
-    }
+// a free slot (not decoding, nobody copying out of it), or -1
+int free_slot(const ChunkService &svc) {
+    for (int i = 0; i < kChunkSlots; i++)
+        if (!svc.slot[i].busy && svc.slot[i].readers == 0) return i;
+    return -1;
+}
+
+// the batching rule: a launch when nothing decodes, or a full enough queue beside a running one
+bool may_lead(const ChunkService &svc) {
+    return !svc.pending.empty() && (svc.in_flight == 0 || svc.pending.size() >= kMinSecond);
+}
+
+// Lead one launch of the queued requests on slot i (lk held on entry and on return, released
+// while the launch runs).  Every request of the batch is marked done; a decoded one holds a reader
+// on the slot until its results are copied out.
+void lead(ppg_ctx *ctx, ChunkService &svc, std::unique_lock<std::mutex> &lk, int i) {
+    const size_t nb = std::min(svc.pending.size(), kMaxBatch);
+    std::vector<ChunkReq *> batch(svc.pending.begin(), svc.pending.begin() + (ptrdiff_t)nb);
+    svc.pending.erase(svc.pending.begin(), svc.pending.begin() + (ptrdiff_t)nb);
+    ChunkSlot &sl = svc.slot[i];
+    sl.busy = true;
+    svc.in_flight++;
+    svc.launches++;
+    svc.max_batch = std::max<int64_t>(svc.max_batch, (int64_t)batch.size());
     lk.unlock();
-    // copy this chunk out of the slot's pinned results (callers copy in parallel)
+    int rc;
+    try {
+        rc = run_launch(ctx, svc, sl, batch);
+    } catch (const std::bad_alloc &) {   // host vectors: never out through the C ABI, never a stuck slot
+        rc = PPG_MEM_ERROR;
+    } catch (...) {
+        rc = PPG_DEVICE_ERROR;
+    }
+    lk.lock();
+    for (ChunkReq *r : batch) {
+        if (rc != PPG_OK) r->rc = rc;
+        if (r->rc == PPG_OK) {
+            r->slot = i;
+            sl.readers++;
+        }
+        r->done = true;
+    }
+    sl.busy = false;
+    svc.in_flight--;
+    svc.cv.notify_all();
+}
+
+// copy a done request's results out of its slot (callers copy in parallel), release the slot
+int finish(ChunkService &svc, ChunkReq &req, uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs,
+           int64_t rec_cap, int64_t *nrec) {
     int rc = req.rc;
     if (rc == PPG_OK) {
         int64_t len = req.got;
@@ -520,9 +582,99 @@ int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uin
                 else if (req.nrec) memcpy(recs, req.src_recs, 16 * (size_t)req.nrec);
             }
         }
-        lk.lock();
-        if (--svc->slot[req.slot].readers == 0) svc->cv.notify_all();
+        std::lock_guard<std::mutex> lk(svc.mu);
+        if (--svc.slot[req.slot].readers == 0) svc.cv.notify_all();
     }
+    return rc;
+}
+
+// the launcher of asynchronous requests: whenever requests are queued and the batching rule allows,
+// after letting a burst of submissions settle (a caller queueing hundreds of chunks gets them into
+// one launch, not the first few into a launch of their own)
+void worker_loop(ChunkService *svc) {
+    using namespace std::chrono;
+    std::unique_lock<std::mutex> lk(svc->mu);
+    for (;;) {
+        svc->cv.wait(lk, [&] { return svc->stop || (may_lead(*svc) && free_slot(*svc) >= 0); });
+        if (svc->stop) return;
+        while (svc->pending.size() < kMaxBatch && steady_clock::now() - svc->last_submit < microseconds(200))
+            svc->cv.wait_for(lk, microseconds(100));
+        const int i = free_slot(*svc);
+        if (i < 0 || !may_lead(*svc)) continue;
+        lead(svc->ctx, *svc, lk, i);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// README "Decompress" (see the top of this file).  Safe to call from any number of host threads
+// on one ctx at once.
+int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
+                         uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
+                         int64_t *nrec) {
+    if (!ctx || !ix || !slice || k < 0 || (size_t)k + 1 >= ix->pts.size() || !ctx->chunks) return PPG_ARG_ERROR;
+    ChunkService *svc = ctx->chunks;
+    ChunkReq req{ix, k, slice, slice_len};
+    std::unique_lock<std::mutex> lk(svc->mu);
+    svc->calls++;
+    svc->pending.push_back(&req);
+    svc->cv.notify_all();
+    while (!req.done) {
+        const int i = free_slot(*svc);
+        if (i < 0 || !may_lead(*svc)) {
+            svc->cv.wait(lk);
+            continue;
+        }
+        // lead a launch of the queued requests (this one among them, unless another caller took it)
+        lead(ctx, *svc, lk, i);
+    }
+    lk.unlock();
+    return finish(*svc, req, out, out_cap, produced, recs, rec_cap, nrec);
+}
+
+int ppg_decompress_chunk_submit(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
+                                uint8_t *out, int64_t out_cap, uint32_t *recs, int64_t rec_cap, ppg_chunk_req **req) {
+    if (!ctx || !ix || !slice || !req || k < 0 || (size_t)k + 1 >= ix->pts.size() || !ctx->chunks) return PPG_ARG_ERROR;
+    ChunkService *svc = ctx->chunks;
+    auto *r = new (std::nothrow) ChunkReq{ix, k, slice, slice_len};
+    if (!r) return PPG_MEM_ERROR;
+    r->async = true;
+    r->out = out;
+    r->out_cap = out_cap;
+    r->recs = recs;
+    r->rec_cap = rec_cap;
+    {
+        std::lock_guard<std::mutex> lk(svc->mu);
+        if (!svc->worker.joinable()) {
+            svc->ctx = ctx;
+            try {
+                svc->worker = std::thread(worker_loop, svc);
+            } catch (...) {
+                delete r;
+                return PPG_MEM_ERROR;
+            }
+        }
+        svc->calls++;
+        svc->pending.push_back(r);
+        svc->last_submit = std::chrono::steady_clock::now();
+    }
+    svc->cv.notify_all();
+    *req = (ppg_chunk_req *)r;
+    return PPG_OK;
+}
+
+int ppg_decompress_chunk_wait(ppg_ctx *ctx, ppg_chunk_req *ticket, int64_t *produced, int64_t *nrec) {
+    if (!ctx || !ticket || !ctx->chunks) return PPG_ARG_ERROR;
+    ChunkService *svc = ctx->chunks;
+    ChunkReq *r = (ChunkReq *)ticket;
+    {
+        std::unique_lock<std::mutex> lk(svc->mu);
+        svc->cv.wait(lk, [&] { return r->done; });
+    }
+    const int rc = finish(*svc, *r, r->out, r->out_cap, produced, r->recs, r->rec_cap, nrec);
+    delete r;
     return rc;
 }
 

@@ -93,7 +93,7 @@ static_assert(sizeof(ShmHdr) <= 64, "header fits the segment's first 64 bytes");
 constexpr uint64_t kShmMagic = 0x7070677368636F6Dull;   // "ppgshcom"
 constexpr int64_t kShmSlot = 8 << 20;   // bytes per rank per all-gather (1M chunk counts)
 constexpr int kShmTimeoutS = 300;
-constexpr size_t kStatSlots = 8;        // int64 per rank in the buffer made with an RCCL comm (status gathers)
+constexpr size_t kStatSlots = 64;       // int64 per rank in the buffer made with an RCCL comm (status and per-peer size gathers)
 
 }  // namespace
 
@@ -453,7 +453,7 @@ int ppg_dist_decompress_all(ppg_ctx *ctx, ppg_comm *comm, const ppg_index *ix, c
 int comm_size(const ppg_comm *c, int32_t *rank, int32_t *nranks) { return ppg_comm_rank(c, rank, nranks); }
 int comm_device(const ppg_comm *c) { return c->host() ? -1 : c->device; }
 
-// All-gather of n <= 8 int64 per rank (statuses and counts), host memory in and out, over either
+// All-gather of n <= 64 int64 per rank (statuses, counts, per-peer sizes), host memory in and out, over either
 // transport, from a buffer made with the comm (nothing to allocate, so every rank always joins).
 // sent_ok reports a failed copy into the collective (the others then got stale data).
 int comm_all_gather_i64(ppg_comm *c, const int64_t *send, int64_t *recv, size_t n, bool &sent_ok) {

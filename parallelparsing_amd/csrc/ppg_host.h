@@ -193,6 +193,9 @@ struct ppg_shard {
     DevBuf<PpgInflateResult> sres;
     DevBuf<uint32_t> sidx;                      // chunk k = sub-jobs [sidx[k], sidx[k+1])
     std::vector<uint32_t> h_sidx;
+    bool lpt = false;                           // the launch runs ljobs: sub-jobs longest first per batch,
+    DevBuf<PpgInflateJob> ljobs;                // results in that order, sub-job j's at linv[j]
+    DevBuf<uint32_t> linv;
 };
 
 // one chunk of a shard: its Points, its window and where file byte from.Input-1 sits in comp

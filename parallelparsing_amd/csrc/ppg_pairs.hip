@@ -21,6 +21,7 @@
 //   compare   ppg_pair_compare counts pairs whose keys differ or are missing (< 0) and finds the
 //             first one; the counts of the two files must agree too.
 #include "ppg_host.h"
+#include <chrono>
 
 namespace {
 constexpr int64_t kDupKey = -2;   // ppg_record_keys: a record the reference parses twice (Q1)
@@ -80,16 +81,133 @@ extern "C" __global__ __launch_bounds__(256) void ppg_pair_compare(const int64_t
     }
 }
 
+// ---- record-aligned pair chunks: records packed back to back (ppg_pairs_emit_*) ----
+// A segment is a run of consecutive records of one chunk's raw text (raw = offset_k ++ body_k, the
+// CombinedMemory of Parsing.cs:72-117), copied to dst + dst with its descriptors rebased by delta.
+struct PpgPackSeg {
+    const uint8_t *off;       // raw [0, olen): the Point's offset carry (may be null when olen = 0)
+    const uint8_t *body;      // raw [olen, ...): the chunk's output (a 64-B readable tail follows)
+    const uint32_t *desc;     // the segment's first record's descriptor (n1, n2, n3, n4)
+    uint64_t olen;
+    uint64_t a, b;            // raw bytes [a, b): ppg_seg_bounds fills them
+    uint64_t dst;             // byte offset in the destination
+    uint64_t ddst;            // record offset in the destination's descriptors
+    uint32_t nrec, first;     // first: the segment starts at its raw's first byte (a = 0)
+    int64_t delta;            // added to every descriptor value: the bytes' offset in their half, - a
+};
+
+// a = the segment's first byte (0, or the previous record's n4 + 1), b = its last record's n4 + 1
+extern "C" __global__ __launch_bounds__(256) void ppg_seg_bounds(PpgPackSeg *__restrict__ seg, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    PpgPackSeg &s = seg[i];
+    s.a = s.first ? 0u : (uint64_t)s.desc[-1] + 1u;
+    s.b = s.nrec ? (uint64_t)s.desc[4 * (uint64_t)s.nrec - 1] + 1u : s.a;
+}
+
+__device__ __forceinline__ uint32_t seg_raw(const PpgPackSeg &s, uint64_t i) {
+    return i < s.olen ? s.off[i] : s.body[i - s.olen];
+}
+
+// grid (x: stripes of a segment, y: segments); 16-B destination words inside the body part from
+// aligned dword loads (alignbyte), the rest -- the offset carry part, an unaligned head and tail --
+// byte by byte (each destination byte belongs to exactly one segment)
+extern "C" __global__ __launch_bounds__(256) void ppg_pack_segs(const PpgPackSeg *__restrict__ seg, int n,
+                                                                uint8_t *__restrict__ dst, uint32_t *__restrict__ ddesc) {
+    for (int y = blockIdx.y; y < n; y += gridDim.y) {
+        const PpgPackSeg s = seg[y];
+        const uint64_t len = s.b - s.a, d0 = s.dst;
+        // bytes: raw [a, b) -> dst [d0, d0 + len); body bytes start at destination bd
+        const uint64_t bd = d0 + (s.olen > s.a ? s.olen - s.a : 0);
+        const uint64_t w0 = (bd + 15) / 16, w1 = (d0 + len) / 16;
+        const uint64_t nw = w1 > w0 ? w1 - w0 : 0;
+        const uint64_t per = (nw + gridDim.x - 1) / gridDim.x;
+        const uint64_t wa = w0 + min(nw, (uint64_t)blockIdx.x * per), wz = w0 + min(nw, (uint64_t)(blockIdx.x + 1) * per);
+        const uint64_t body_a = s.a > s.olen ? s.a - s.olen : 0;   // body byte at destination bd
+        for (uint64_t w = wa + threadIdx.x; w < wz; w += 256) {
+            const uint8_t *src = s.body + body_a + (16 * w - bd);
+            const uint32_t *s32 = (const uint32_t *)((uintptr_t)src & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+            const uint32_t x0 = s32[0], x1 = s32[1], x2 = s32[2], x3 = s32[3], x4 = s32[4];
+            uint4 v;
+            v.x = __builtin_amdgcn_alignbyte(x1, x0, sh);
+            v.y = __builtin_amdgcn_alignbyte(x2, x1, sh);
+            v.z = __builtin_amdgcn_alignbyte(x3, x2, sh);
+            v.w = __builtin_amdgcn_alignbyte(x4, x3, sh);
+            *(uint4 *)(dst + 16 * w) = v;
+        }
+        if (blockIdx.x == 0) {
+            const uint64_t head = nw ? 16 * w0 - d0 : len;
+            for (uint64_t i = threadIdx.x; i < head; i += 256) dst[d0 + i] = (uint8_t)seg_raw(s, s.a + i);
+            if (nw)
+                for (uint64_t i = 16 * w1 - d0 + threadIdx.x; i < len; i += 256) dst[d0 + i] = (uint8_t)seg_raw(s, s.a + i);
+        }
+        // descriptors, rebased (u32 arithmetic: a half stays under 4 GiB)
+        const uint64_t nv = 4 * (uint64_t)s.nrec;
+        const uint64_t pv = (nv + gridDim.x - 1) / gridDim.x;
+        const uint64_t va = min(nv, (uint64_t)blockIdx.x * pv), vz = min(nv, (uint64_t)(blockIdx.x + 1) * pv);
+        for (uint64_t i = va + threadIdx.x; i < vz; i += 256)
+            ddesc[4 * s.ddst + i] = (uint32_t)((int64_t)s.desc[i] + s.delta);
+    }
+}
+
 hipError_t ppg_launch_record_keys(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   const PpgParseInfo *info, const uint64_t *base, const uint32_t *recs, int64_t *keys,
                                   int n);
+
+// a shard's state around a batch run again for emission (rerun_launch / rerun_collect)
+struct RerunSave {
+    int64_t tot = 0;
+    float ti = 0, tp = 0, tt = 0;
+    int64_t *keys = nullptr;
+};
+
+// ppg_pairs_emit_*: the record-aligned pair chunks (see the ABI comment in include/ppgpu.h)
+struct PairEmit {
+    bool on = false;
+    int64_t K = 0, npc = 0;                 // pair chunk size; pair chunks in all
+    int64_t j_lo = 0, j_hi = 0;             // this rank's pair chunks
+    int64_t next = 0;                       // the next window's first pair chunk
+    int64_t w0 = 0, w1 = 0;                 // the current window
+    int64_t window_bytes = 0;               // one rank: bytes per window and file (a budget, >= 1 pair chunk)
+    ppg_shard *sh[2] = {nullptr, nullptr};
+    ppg_comm *comm = nullptr;
+    bool exchanged = false;                 // N ranks: the one window is done
+    int32_t batch[2] = {-1, -1};            // one rank: the resident output batch of each shard
+    std::vector<int64_t> blo[2], bhi[2];    // one rank: each batch's deduplicated record range
+    std::vector<uint64_t> offst[2];         // chunk k's offset carry in sh->offs
+    std::vector<int64_t> pos[2];            // shard positions of the duplicates (sorted)
+    // the current window: per pair chunk j (from w0) and file, byte offset / length, first record / count
+    std::vector<int64_t> boff[2], blen[2], roff[2], rcnt[2];
+    DevBuf<uint8_t> bytes[2];
+    DevBuf<uint32_t> desc[2];
+    // one rank: the part of pair chunk `next` carried from an earlier batch
+    DevBuf<uint8_t> cbytes[2];
+    DevBuf<uint32_t> cdesc[2];
+    int64_t clen[2] = {0, 0}, cnrec[2] = {0, 0};
+    DevBuf<PpgPackSeg> dseg;
+    // N ranks: exchange buffers (bytes as int64 words, descriptors as two int64 per record)
+    DevBuf<int64_t> sbuf[2], rbuf[2], sdesc[2], rdesc[2];
+    RerunSave save[2];
+    double t_ms[4] = {0, 0, 0, 0};          // batches re-run, packing, exchange, total (ms, cumulative)
+    int64_t reruns = 0;
+    void release() {
+        for (int f = 0; f < 2; f++) {
+            bytes[f].release(); desc[f].release(); cbytes[f].release(); cdesc[f].release();
+            sbuf[f].release(); rbuf[f].release(); sdesc[f].release(); rdesc[f].release();
+        }
+        dseg.release();
+    }
+};
 
 struct ppg_pairs {
     int device = -1;
     int32_t rank = 0, nranks = 1;
     int64_t local[2] = {0, 0}, start[2] = {0, 0};   // deduplicated records of this rank / before it
     std::vector<int64_t> dp[2];                     // D[t] - t of the sorted duplicate positions
+    std::vector<int64_t> st[2];                     // N ranks: deduplicated records before rank r (r = 0..R)
+    PairEmit em;
     ppg_pair_result res{};
     bool checked = false;
     // device scratch, kept across checks (grow only)
@@ -102,6 +220,7 @@ struct ppg_pairs {
     DevBuf<unsigned long long> dres;
     void release() {
         for (int f = 0; f < 2; f++) { keys[f].release(); dkeys[f].release(); own[f].release(); }
+        em.release();
         dpos.release();
         ddp.release();
         dcount.release();
@@ -243,6 +362,8 @@ static int check_dist(ppg_pairs *p, ppg_comm *comm, const int64_t *k[2], int sta
     for (int32_t r = 0; r <= R; r++) own[(size_t)r] = (int64_t)((__int128)pairs * r / R);
     p->start[0] = st[0][(size_t)me];
     p->start[1] = st[1][(size_t)me];
+    p->st[0] = st[0];
+    p->st[1] = st[1];
     const int64_t mine_pairs = own[(size_t)me + 1] - own[(size_t)me];
     // phase 2: every key to the rank that owns its pair number, one all-to-all-v per file (the keys
     // a rank sends are its deduplicated ones below `pairs`, compacted first; every rank agrees that
@@ -299,6 +420,467 @@ static int check_dist(ppg_pairs *p, ppg_comm *comm, const int64_t *k[2], int sta
     if (Rz.first_bad < 0 && Rz.mismatches) Rz.first_bad = pairs;
     return PPG_OK;
 }
+
+// ================= record-aligned pair chunks (ppg_pairs_emit_*, include/ppgpu.h) =================
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// shard record number of this rank's deduplicated record d (skip the duplicates at or before it)
+int64_t shard_rec(const std::vector<int64_t> &dp, int64_t d) {
+    return d + (int64_t)(std::upper_bound(dp.begin(), dp.end(), d) - dp.begin());
+}
+// deduplicated number of the first record at or after shard record r
+int64_t dedup_of(const std::vector<int64_t> &pos, int64_t r) {
+    return r - (int64_t)(std::lower_bound(pos.begin(), pos.end(), r) - pos.begin());
+}
+
+// where a segment of records lands: the segment list is built first, placed once their byte spans are known
+struct SegPlace {
+    int32_t grp;        // destination group (a pair chunk half, or an exchange piece)
+};
+
+// The runs of consecutive records of this rank's deduplicated records [d0, d1) of file f, split at
+// chunk boundaries and at the duplicates, from the shard's resident output batch
+void make_segs(const ppg_pairs *p, int f, int64_t d0, int64_t d1, int32_t grp, std::vector<PpgPackSeg> &seg,
+               std::vector<SegPlace> &pl) {
+    const PairEmit &E = p->em;
+    const ppg_shard *sh = E.sh[f];
+    const auto &B = sh->h_base;
+    const auto &pos = E.pos[f];
+    int64_t d = d0;
+    while (d < d1) {
+        const int64_t r = shard_rec(p->dp[f], d);
+        const int32_t k = (int32_t)(std::upper_bound(B.begin(), B.end(), r) - B.begin()) - 1;
+        const int64_t cend = B[(size_t)k] + (int64_t)sh->h_info[(size_t)k].records;
+        const auto nd = std::upper_bound(pos.begin(), pos.end(), r);
+        const int64_t stop = std::min<int64_t>(cend, nd == pos.end() ? INT64_MAX : *nd);
+        const int64_t run = std::min(stop - r, d1 - d);
+        const PpgInflateJob &J = sh->h_jobs[(size_t)k];
+        PpgPackSeg g{};
+        g.off = sh->offs.p + E.offst[f][(size_t)k];
+        g.olen = J.raw_shift;
+        g.body = sh->out.p + J.out_off;
+        g.desc = sh->recs.p + 4 * r;
+        g.nrec = (uint32_t)run;
+        g.first = r == B[(size_t)k] ? 1u : 0u;
+        seg.push_back(g);
+        pl.push_back(SegPlace{grp});
+        d += run;
+    }
+}
+
+template <class B>
+int grow_keep(B &b, size_t need, hipStream_t s, size_t keep) {   // grow, keeping the first `keep` elements
+    if (b.p && b.n >= need) return PPG_OK;
+    B g;
+    HIPCHK(g.alloc(std::max(need, b.n + b.n / 2)));
+    if (keep) HIPCHK(hipMemcpyAsync(g.p, b.p, keep * sizeof(*b.p), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::swap(g.p, b.p);
+    std::swap(g.n, b.n);
+    return PPG_OK;
+}
+
+// fill a, b of every segment (their first and last records' descriptors), on the device
+int seg_bounds(PairEmit &E, std::vector<PpgPackSeg> &seg, hipStream_t s) {
+    if (seg.empty()) return PPG_OK;
+    HIPCHK(grow(E.dseg, seg.size()));
+    HIPCHK(hipMemcpyAsync(E.dseg.p, seg.data(), sizeof(PpgPackSeg) * seg.size(), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(ppg_seg_bounds, dim3((unsigned)((seg.size() + 255) / 256)), dim3(256), 0, s, E.dseg.p, (int)seg.size());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(seg.data(), E.dseg.p, sizeof(PpgPackSeg) * seg.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return PPG_OK;
+}
+
+// copy the placed segments (dst, ddst, delta set) into dst / ddesc
+int seg_pack(PairEmit &E, const std::vector<PpgPackSeg> &seg, uint8_t *dst, uint32_t *ddesc, hipStream_t s) {
+    if (seg.empty()) return PPG_OK;
+    HIPCHK(grow(E.dseg, seg.size()));
+    HIPCHK(hipMemcpyAsync(E.dseg.p, seg.data(), sizeof(PpgPackSeg) * seg.size(), hipMemcpyHostToDevice, s));
+    uint64_t mx = 0;
+    for (const auto &g : seg) mx = std::max<uint64_t>(mx, g.b - g.a);
+    const unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(64, mx / 65536 + 1));
+    const unsigned gy = (unsigned)std::min<size_t>(seg.size(), 65535);
+    hipLaunchKernelGGL(ppg_pack_segs, dim3(gx, gy), dim3(256), 0, s, E.dseg.p, (int)seg.size(), dst, ddesc);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));   // the host segment list and dseg are reused
+    return PPG_OK;
+}
+
+// batch b of a shard's batches run again, its output resident (one rank: the windows advance over
+// the batches): launch, then collect (two shards' batches are in flight together); the shard's
+// record totals, bases, keys and timing are left as its run left them
+int rerun_launch(ppg_shard *sh, int32_t b, RerunSave &sv) {
+    const auto [b0, b1] = sh->batches[(size_t)b];
+    sv = RerunSave{sh->total_records, sh->t_inflate, sh->t_parse, sh->t_total, sh->keys_dev};
+    sh->total_records = sh->h_base[(size_t)b0];   // descriptors rewritten where the run wrote them
+    sh->keys_dev = nullptr;
+    const int rc = batch_launch(sh, b0, b1);
+    if (rc != PPG_OK) {
+        sh->total_records = sv.tot;
+        sh->keys_dev = sv.keys;
+    }
+    return rc;
+}
+
+int rerun_collect(ppg_shard *sh, int32_t b, const RerunSave &sv) {
+    const auto [b0, b1] = sh->batches[(size_t)b];
+    float ms = 0;
+    const int rc = batch_collect(sh, b0, b1, ms);
+    sh->total_records = sv.tot;
+    sh->t_inflate = sv.ti;
+    sh->t_parse = sv.tp;
+    sh->t_total = sv.tt;
+    sh->keys_dev = sv.keys;
+    return rc;
+}
+
+// ---- one rank: windows over the shards' batches ----
+int emit_next_local(ppg_pairs *p, int64_t *j0, int64_t *j1) {
+    PairEmit &E = p->em;
+    const int64_t K = E.K, pairs = p->res.pairs, e = E.next;
+    if (e >= E.j_hi) return PPG_STREAM_END;
+    const auto t0 = Clock::now();
+    // 1. each file's resident batch must complete pair chunk e; a batch holding only its first part
+    //    hands that part to the carry first (the next batch's run overwrites the output).  Both
+    //    files' batches run together, each on its shard's own stream.
+    const int64_t need = std::min((e + 1) * K, pairs);
+    for (;;) {
+        bool run[2] = {false, false};
+        for (int f = 0; f < 2; f++) {
+            ppg_shard *sh = E.sh[f];
+            const int64_t cend = e * K + E.cnrec[f];
+            const int32_t b = E.batch[f];
+            if (E.blo[f][(size_t)b] <= cend && E.bhi[f][(size_t)b] >= need) continue;
+            hipStream_t s = shard_stream(sh);
+            if (E.blo[f][(size_t)b] <= cend && cend < E.bhi[f][(size_t)b]) {
+                std::vector<PpgPackSeg> seg;
+                std::vector<SegPlace> pl;
+                make_segs(p, f, cend, E.bhi[f][(size_t)b], 0, seg, pl);
+                if (int rc = seg_bounds(E, seg, s)) return rc;
+                int64_t add = 0, nadd = 0;
+                for (auto &g : seg) {
+                    g.dst = (uint64_t)(E.clen[f] + add);
+                    g.ddst = (uint64_t)(E.cnrec[f] + nadd);
+                    g.delta = (int64_t)g.dst - (int64_t)g.a;   // the carry starts its half
+                    add += (int64_t)(g.b - g.a);
+                    nadd += g.nrec;
+                }
+                if (int rc = grow_keep(E.cbytes[f], (size_t)(E.clen[f] + add) + 64, s, (size_t)E.clen[f])) return rc;
+                if (int rc = grow_keep(E.cdesc[f], 4 * (size_t)(E.cnrec[f] + nadd) + 4, s, 4 * (size_t)E.cnrec[f])) return rc;
+                if (int rc = seg_pack(E, seg, E.cbytes[f].p, E.cdesc[f].p, s)) return rc;
+                E.clen[f] += add;
+                E.cnrec[f] += nadd;
+            }
+            // the batch holding the carry's end
+            const int64_t c2 = e * K + E.cnrec[f];
+            int32_t nb = 0;
+            while ((size_t)nb + 1 < E.bhi[f].size() && E.bhi[f][(size_t)nb] <= c2) nb++;
+            if (nb == b) return PPG_DATA_ERROR;   // no progress: the batches cannot complete the pair chunk
+            E.batch[f] = nb;
+            run[f] = true;
+        }
+        if (!run[0] && !run[1]) break;
+        const auto tr = Clock::now();
+        int rc = PPG_OK;
+        bool launched[2] = {false, false};
+        for (int f = 0; f < 2 && rc == PPG_OK; f++)
+            if (run[f]) {
+                rc = rerun_launch(E.sh[f], E.batch[f], E.save[f]);
+                launched[f] = rc == PPG_OK;
+            }
+        for (int f = 0; f < 2; f++)
+            if (launched[f]) {
+                const int x = rerun_collect(E.sh[f], E.batch[f], E.save[f]);
+                if (rc == PPG_OK) rc = x;
+            }
+        if (rc != PPG_OK) return rc;
+        E.reruns += run[0] + run[1];
+        E.t_ms[0] += ms_since(tr);
+    }
+    // 2. the window: the pair chunks both resident batches complete, within the byte budget
+    int64_t J = E.j_hi;
+    for (int f = 0; f < 2; f++) {
+        const int64_t hi = E.bhi[f][(size_t)E.batch[f]];
+        if (hi < pairs) J = std::min(J, hi / K);
+    }
+    if (J <= e) return PPG_DATA_ERROR;
+    const auto tp = Clock::now();
+    std::vector<PpgPackSeg> seg[2];
+    std::vector<SegPlace> pl[2];
+    for (int f = 0; f < 2; f++) {
+        for (int64_t j = e; j < J; j++) {
+            const int64_t a = j == e ? e * K + E.cnrec[f] : j * K, z = std::min((j + 1) * K, pairs);
+            make_segs(p, f, a, z, (int32_t)(j - e), seg[f], pl[f]);
+        }
+        if (int rc = seg_bounds(E, seg[f], shard_stream(E.sh[f]))) return rc;
+    }
+    // cut the window where either file's halves pass the byte budget (one pair chunk at least)
+    std::vector<int64_t> hb[2];
+    for (int f = 0; f < 2; f++) {
+        hb[f].assign((size_t)(J - e), 0);
+        hb[f][0] = E.clen[f];
+        for (size_t i = 0; i < seg[f].size(); i++) hb[f][(size_t)pl[f][i].grp] += (int64_t)(seg[f][i].b - seg[f][i].a);
+    }
+    int64_t J2 = e + 1;
+    {
+        int64_t acc[2] = {(hb[0][0] + 15) / 16 * 16, (hb[1][0] + 15) / 16 * 16};
+        while (J2 < J) {
+            const size_t i = (size_t)(J2 - e);
+            if (acc[0] + hb[0][i] > E.window_bytes || acc[1] + hb[1][i] > E.window_bytes) break;
+            acc[0] += (hb[0][i] + 15) / 16 * 16;
+            acc[1] += (hb[1][i] + 15) / 16 * 16;
+            J2++;
+        }
+    }
+    // 3. place and pack both files' halves of pair chunks [e, J2)
+    for (int f = 0; f < 2; f++) {
+        hipStream_t s = shard_stream(E.sh[f]);
+        const size_t nj = (size_t)(J2 - e);
+        E.boff[f].assign(nj, 0);
+        E.blen[f].assign(nj, 0);
+        E.roff[f].assign(nj, 0);
+        E.rcnt[f].assign(nj, 0);
+        int64_t bo = 0, ro = 0;
+        for (size_t i = 0; i < nj; i++) {
+            E.boff[f][i] = bo;
+            E.roff[f][i] = ro;
+            E.blen[f][i] = hb[f][i];
+            const int64_t lo = i == 0 ? e * K : (e + (int64_t)i) * K, z = std::min((e + (int64_t)i + 1) * K, pairs);
+            E.rcnt[f][i] = z - lo;
+            bo += (hb[f][i] + 15) / 16 * 16;
+            ro += E.rcnt[f][i];
+        }
+        if (int rc = grow_keep(E.bytes[f], (size_t)bo + 64, s, 0)) return rc;
+        if (int rc = grow_keep(E.desc[f], 4 * (size_t)ro + 4, s, 0)) return rc;
+        // the carried first part of pair chunk e (its descriptors are relative to the half already)
+        if (E.cnrec[f]) {
+            HIPCHK(hipMemcpyAsync(E.bytes[f].p, E.cbytes[f].p, (size_t)E.clen[f], hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(E.desc[f].p, E.cdesc[f].p, 16 * (size_t)E.cnrec[f], hipMemcpyDeviceToDevice, s));
+        }
+        std::vector<int64_t> at(nj, 0), rat(nj, 0);
+        at[0] = E.clen[f];
+        rat[0] = E.cnrec[f];
+        std::vector<PpgPackSeg> go;
+        for (size_t i = 0; i < seg[f].size(); i++) {
+            const size_t g = (size_t)pl[f][i].grp;
+            if (g >= nj) break;
+            PpgPackSeg x = seg[f][i];
+            x.dst = (uint64_t)(E.boff[f][g] + at[g]);
+            x.ddst = (uint64_t)(E.roff[f][g] + rat[g]);
+            x.delta = at[g] - (int64_t)x.a;
+            at[g] += (int64_t)(x.b - x.a);
+            rat[g] += x.nrec;
+            go.push_back(x);
+        }
+        if (int rc = seg_pack(E, go, E.bytes[f].p, E.desc[f].p, s)) return rc;
+        E.clen[f] = E.cnrec[f] = 0;
+    }
+    E.t_ms[1] += ms_since(tp);
+    E.w0 = e;
+    E.w1 = J2;
+    E.next = J2;
+    E.t_ms[3] += ms_since(t0);
+    if (j0) *j0 = e;
+    if (j1) *j1 = J2;
+    return PPG_OK;
+}
+
+// ---- N ranks: one window, the records this rank does not hold moved over the comm ----
+int emit_exchange(ppg_pairs *p, int64_t *j0, int64_t *j1) {
+    PairEmit &E = p->em;
+    const int32_t R = p->nranks, me = p->rank;
+    const int64_t K = E.K, pairs = p->res.pairs;
+    const auto t0 = Clock::now();
+    // ownership: rank r owns the pair chunks that start in its R1 range
+    std::vector<int64_t> jr((size_t)R + 1);
+    for (int32_t r = 0; r < R; r++) jr[(size_t)r] = std::min(E.npc, (p->st[0][(size_t)r] + K - 1) / K);
+    jr[(size_t)R] = E.npc;
+    for (int32_t r = 1; r <= R; r++) jr[(size_t)r] = std::max(jr[(size_t)r], jr[(size_t)r - 1]);
+    auto own_lo = [&](int32_t r) { return std::min(jr[(size_t)r] * K, pairs); };
+    auto own_hi = [&](int32_t r) { return std::min(jr[(size_t)r + 1] * K, pairs); };
+    E.j_lo = jr[(size_t)me];
+    E.j_hi = jr[(size_t)me + 1];
+    int status = PPG_OK;
+    hipStream_t s = shard_stream(E.sh[0]);
+    // 1. this rank's records to each owner: one piece per (owner, pair chunk), packed by owner
+    std::vector<int64_t> sendw[2];   // per owner: int64 words of bytes
+    std::vector<int64_t> piece_len[2];
+    for (int f = 0; f < 2 && status == PPG_OK; f++) {
+        sendw[f].assign((size_t)R, 0);
+        const int64_t h0 = p->st[f][(size_t)me], h1 = p->st[f][(size_t)me + 1];
+        std::vector<PpgPackSeg> seg;
+        std::vector<SegPlace> pl;
+        std::vector<int32_t> pdst;   // owner of each piece
+        int32_t np = 0;
+        for (int32_t r = 0; r < R; r++) {
+            const int64_t a = std::max(h0, own_lo(r)), z = std::min(h1, own_hi(r));
+            for (int64_t lo = a; lo < z;) {
+                const int64_t hi = std::min(z, (lo / K + 1) * K);
+                make_segs(p, f, lo - h0, hi - h0, np++, seg, pl);
+                pdst.push_back(r);
+                lo = hi;
+            }
+        }
+        status = seg_bounds(E, seg, s);
+        if (status != PPG_OK) break;
+        piece_len[f].assign((size_t)np, 0);
+        std::vector<int64_t> piece_rec((size_t)np, 0);
+        for (size_t i = 0; i < seg.size(); i++) {
+            piece_len[f][(size_t)pl[i].grp] += (int64_t)(seg[i].b - seg[i].a);
+            piece_rec[(size_t)pl[i].grp] += seg[i].nrec;
+        }
+        // owner groups: pieces back to back, each group padded to 8 bytes (int64 words)
+        std::vector<int64_t> poff((size_t)np), proff((size_t)np);
+        int64_t gb = 0, gr = 0;
+        for (int32_t r = 0, i = 0; r < R; r++) {
+            const int64_t start = gb;
+            for (; i < np && pdst[(size_t)i] == r; i++) {
+                poff[(size_t)i] = gb;
+                proff[(size_t)i] = gr;
+                gb += piece_len[f][(size_t)i];
+                gr += piece_rec[(size_t)i];
+            }
+            gb = (gb + 7) / 8 * 8;
+            sendw[f][(size_t)r] = (gb - start) / 8;
+        }
+        std::vector<int64_t> at((size_t)np, 0), rat((size_t)np, 0);
+        for (size_t i = 0; i < seg.size(); i++) {
+            const size_t g = (size_t)pl[i].grp;
+            seg[i].dst = (uint64_t)(poff[g] + at[g]);
+            seg[i].ddst = (uint64_t)(proff[g] + rat[g]);
+            seg[i].delta = at[g] - (int64_t)seg[i].a;   // descriptors relative to their piece
+            at[g] += (int64_t)(seg[i].b - seg[i].a);
+            rat[g] += seg[i].nrec;
+        }
+        if (grow(E.sbuf[f], (size_t)gb / 8 + 8) != hipSuccess || grow(E.sdesc[f], 2 * (size_t)gr + 2) != hipSuccess) {
+            status = PPG_MEM_ERROR;
+            break;
+        }
+        status = seg_pack(E, seg, (uint8_t *)E.sbuf[f].p, (uint32_t *)E.sdesc[f].p, s);
+    }
+    // 2. every rank's status and per-owner word counts (both files), then the exchanges
+    std::vector<int64_t> mine(1 + 2 * (size_t)R, 0), all((1 + 2 * (size_t)R) * R, 0);
+    mine[0] = status;
+    for (int f = 0; f < 2; f++)
+        for (int32_t r = 0; r < R; r++) mine[1 + (size_t)f * R + r] = sendw[f].empty() ? 0 : sendw[f][(size_t)r];
+    bool sent_ok = true;
+    const auto tx = Clock::now();
+    if (int g = comm_all_gather_i64(E.comm, mine.data(), all.data(), mine.size(), sent_ok)) return g;
+    for (int32_t r = 0; r < R; r++)
+        if (all[(size_t)r * mine.size()] != PPG_OK) return (int)all[(size_t)r * mine.size()];
+    if (!sent_ok) return PPG_DEVICE_ERROR;
+    int rc = PPG_OK;
+    std::vector<int64_t> mw[2], md[2];
+    for (int f = 0; f < 2; f++) {
+        mw[f].assign((size_t)R * R, 0);
+        md[f].assign((size_t)R * R, 0);
+        for (int32_t q = 0; q < R; q++)
+            for (int32_t r = 0; r < R; r++) {
+                mw[f][(size_t)q * R + r] = all[(size_t)q * mine.size() + 1 + (size_t)f * R + r];
+                const int64_t a = std::max(p->st[f][(size_t)q], own_lo(r)), z = std::min(p->st[f][(size_t)q + 1], own_hi(r));
+                md[f][(size_t)q * R + r] = 2 * std::max<int64_t>(0, z - a);
+            }
+        int64_t rw = 0, rdn = 0;
+        for (int32_t q = 0; q < R; q++) {
+            rw += mw[f][(size_t)q * R + me];
+            rdn += md[f][(size_t)q * R + me];
+        }
+        if (rc == PPG_OK && (grow(E.rbuf[f], (size_t)rw + 8) != hipSuccess || grow(E.rdesc[f], (size_t)rdn + 2) != hipSuccess))
+            rc = PPG_MEM_ERROR;
+    }
+    {   // agree that every rank has its receive buffers before moving anything
+        int64_t st1 = rc;
+        std::vector<int64_t> v((size_t)R, 0);
+        if (int g = comm_all_gather_i64(E.comm, &st1, v.data(), 1, sent_ok)) return g;
+        for (int32_t r = 0; r < R; r++)
+            if (v[(size_t)r] != PPG_OK) return (int)v[(size_t)r];
+        if (!sent_ok) return PPG_DEVICE_ERROR;
+    }
+    for (int f = 0; f < 2; f++) {
+        const int x = comm_alltoallv_i64(E.comm, s, E.sbuf[f].p, E.rbuf[f].p, mw[f].data(), true);
+        const int y = comm_alltoallv_i64(E.comm, s, E.sdesc[f].p, E.rdesc[f].p, md[f].data(), true);
+        if (rc == PPG_OK) rc = x != PPG_OK ? x : y;
+    }
+    E.t_ms[2] += ms_since(tx);
+    if (rc != PPG_OK) return rc;
+    // 3. the received pieces, source by source, into this rank's pair chunk halves
+    const int64_t nj = E.j_hi - E.j_lo;
+    for (int f = 0; f < 2; f++) {
+        std::vector<PpgPackSeg> seg;
+        std::vector<int64_t> pj;    // pair chunk (from j_lo) of each piece
+        int64_t wq = 0, rq = 0;     // source group starts (words, records)
+        for (int32_t q = 0; q < R; q++) {
+            const int64_t a = std::max(p->st[f][(size_t)q], own_lo(me)), z = std::min(p->st[f][(size_t)q + 1], own_hi(me));
+            int64_t rr = rq;
+            for (int64_t lo = a; lo < z;) {
+                const int64_t hi = std::min(z, (lo / K + 1) * K);
+                PpgPackSeg g{};
+                g.desc = (const uint32_t *)E.rdesc[f].p + 4 * rr;
+                g.nrec = (uint32_t)(hi - lo);
+                g.first = 1;
+                g.body = (const uint8_t *)(E.rbuf[f].p + wq);   // + the piece's offset in its group (below)
+                seg.push_back(g);
+                pj.push_back(lo / K - E.j_lo);
+                rr += hi - lo;
+                lo = hi;
+            }
+            wq += mw[f][(size_t)q * R + me];
+            rq += md[f][(size_t)q * R + me] / 2;
+        }
+        if (int x = seg_bounds(E, seg, s)) return x;   // b = the piece's length (a = 0)
+        // bodies: pieces of one source group back to back
+        {
+            const uint8_t *grp = nullptr;
+            uint64_t run = 0;
+            for (auto &g : seg) {
+                if (g.body != grp) { grp = g.body; run = 0; }
+                g.body = grp + run;
+                run += g.b;
+            }
+        }
+        E.boff[f].assign((size_t)nj, 0);
+        E.blen[f].assign((size_t)nj, 0);
+        E.roff[f].assign((size_t)nj, 0);
+        E.rcnt[f].assign((size_t)nj, 0);
+        for (size_t i = 0; i < seg.size(); i++) {
+            E.blen[f][(size_t)pj[i]] += (int64_t)seg[i].b;
+            E.rcnt[f][(size_t)pj[i]] += seg[i].nrec;
+        }
+        int64_t bo = 0, ro = 0;
+        for (int64_t j = 0; j < nj; j++) {
+            E.boff[f][(size_t)j] = bo;
+            E.roff[f][(size_t)j] = ro;
+            bo += (E.blen[f][(size_t)j] + 15) / 16 * 16;
+            ro += E.rcnt[f][(size_t)j];
+        }
+        if (grow(E.bytes[f], (size_t)bo + 64) != hipSuccess || grow(E.desc[f], 4 * (size_t)ro + 4) != hipSuccess)
+            return PPG_MEM_ERROR;
+        std::vector<int64_t> at((size_t)nj, 0), rat((size_t)nj, 0);
+        for (size_t i = 0; i < seg.size(); i++) {
+            const size_t j = (size_t)pj[i];
+            seg[i].dst = (uint64_t)(E.boff[f][j] + at[j]);
+            seg[i].ddst = (uint64_t)(E.roff[f][j] + rat[j]);
+            seg[i].delta = at[j];
+            at[j] += (int64_t)seg[i].b;
+            rat[j] += seg[i].nrec;
+        }
+        if (int x = seg_pack(E, seg, E.bytes[f].p, E.desc[f].p, s)) return x;
+    }
+    E.w0 = E.j_lo;
+    E.w1 = E.j_hi;
+    E.next = E.j_hi;
+    E.exchanged = true;
+    E.t_ms[3] += ms_since(t0);
+    if (j0) *j0 = E.w0;
+    if (j1) *j1 = E.w1;
+    return PPG_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -368,6 +950,112 @@ int ppg_pairs_records(const ppg_pairs *p, int32_t file, int64_t lo, int64_t hi, 
         }
         shard_record[i - lo] = d + (int64_t)(std::upper_bound(dp.begin(), dp.end(), d) - dp.begin());
     }
+    return PPG_OK;
+}
+
+int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *comm, int64_t pair_chunk,
+                         int64_t window_bytes) {
+    if (!p || !p->checked || !r1 || !r2 || pair_chunk < 1) return PPG_ARG_ERROR;
+    int32_t rank = 0, nranks = 1;
+    if (comm) comm_size(comm, &rank, &nranks);
+    if (nranks != p->nranks || rank != p->rank) return PPG_ARG_ERROR;   // the check's comm
+    PairEmit &E = p->em;
+    E.on = false;
+    E.K = pair_chunk;
+    E.npc = (p->res.pairs + pair_chunk - 1) / pair_chunk;
+    E.sh[0] = r1;
+    E.sh[1] = r2;
+    E.comm = comm;
+    E.exchanged = false;
+    E.next = E.w0 = E.w1 = 0;
+    E.window_bytes = window_bytes > 0 ? window_bytes : (int64_t)8 << 30;
+    E.clen[0] = E.clen[1] = E.cnrec[0] = E.cnrec[1] = 0;
+    E.reruns = 0;
+    for (double &t : E.t_ms) t = 0;
+    for (int f = 0; f < 2; f++) {
+        ppg_shard *sh = E.sh[f];
+        if (!sh->ran || sh->last_rc != PPG_OK) return PPG_ARG_ERROR;
+        if (nranks > 1 && sh->batches.size() != 1) return PPG_UNSUPPORTED;   // N ranks: resident shards only
+        E.offst[f].assign((size_t)sh->n, 0);
+        uint64_t o = 0;
+        for (int32_t k = 0; k < sh->n; k++) {
+            E.offst[f][(size_t)k] = o;
+            o += sh->h_jobs[(size_t)k].raw_shift;
+        }
+        E.pos[f].resize(p->dp[f].size());
+        for (size_t t = 0; t < p->dp[f].size(); t++) E.pos[f][t] = p->dp[f][t] + (int64_t)t;
+        // each batch's deduplicated record range
+        E.blo[f].clear();
+        E.bhi[f].clear();
+        for (auto [b0, b1] : sh->batches) {
+            const int64_t r0 = sh->h_base[(size_t)b0], r1e = b1 < sh->n ? sh->h_base[(size_t)b1] : sh->total_records;
+            E.blo[f].push_back(dedup_of(E.pos[f], r0));
+            E.bhi[f].push_back(dedup_of(E.pos[f], r1e));
+        }
+        E.batch[f] = (int32_t)sh->batches.size() - 1;   // what the run left resident
+    }
+    if (nranks == 1) {
+        E.j_lo = 0;
+        E.j_hi = E.npc;
+        // the windows' deduplicated numbering is this rank's: pairs beyond either file's records do not exist
+        for (int f = 0; f < 2; f++)
+            if (E.bhi[f].empty() ? p->res.pairs > 0 : E.bhi[f].back() < p->res.pairs) return PPG_ARG_ERROR;
+    } else {
+        if (p->st[0].size() != (size_t)nranks + 1 || p->st[1].size() != (size_t)nranks + 1) return PPG_ARG_ERROR;
+        E.j_lo = E.j_hi = 0;   // set by the exchange
+    }
+    E.on = true;
+    return PPG_OK;
+}
+
+int ppg_pairs_emit_next(ppg_pairs *p, int64_t *j0, int64_t *j1) {
+    if (!p || !p->em.on) return PPG_ARG_ERROR;
+    HIPCHK(hipSetDevice(p->device));
+    PairEmit &E = p->em;
+    if (p->nranks > 1) {
+        if (E.exchanged) return PPG_STREAM_END;
+        const int rc = emit_exchange(p, j0, j1);
+        if (rc != PPG_OK) { E.on = false; return rc; }
+        return E.w0 < E.w1 ? PPG_OK : PPG_STREAM_END;
+    }
+    const int rc = emit_next_local(p, j0, j1);
+    if (rc < 0) E.on = false;
+    return rc;
+}
+
+int ppg_pairs_chunk(ppg_pairs *p, int64_t j, int32_t file, const uint8_t **bytes, int64_t *len, const uint32_t **desc,
+                    int64_t *nrec) {
+    if (!p || !p->em.on || file < 0 || file > 1 || j < p->em.w0 || j >= p->em.w1) return PPG_ARG_ERROR;
+    const PairEmit &E = p->em;
+    const size_t i = (size_t)(j - E.w0);
+    if (bytes) *bytes = E.bytes[file].p + E.boff[file][i];
+    if (len) *len = E.blen[file][i];
+    if (desc) *desc = E.desc[file].p + 4 * E.roff[file][i];
+    if (nrec) *nrec = E.rcnt[file][i];
+    return PPG_OK;
+}
+
+int ppg_pairs_copy_chunk(ppg_pairs *p, int64_t j, int32_t file, uint8_t *dst, int64_t cap, int64_t *len, uint32_t *desc,
+                         int64_t desc_cap, int64_t *nrec) {
+    const uint8_t *b = nullptr;
+    const uint32_t *d = nullptr;
+    int64_t n = 0, r = 0;
+    if (int rc = ppg_pairs_chunk(p, j, file, &b, &n, &d, &r)) return rc;
+    if (len) *len = n;
+    if (nrec) *nrec = r;
+    if ((dst && n > cap) || (desc && r > desc_cap)) return PPG_BUF_ERROR;
+    HIPCHK(hipSetDevice(p->device));
+    if (dst && n) HIPCHK(hipMemcpy(dst, b, (size_t)n, hipMemcpyDeviceToHost));
+    if (desc && r) HIPCHK(hipMemcpy(desc, d, 16 * (size_t)r, hipMemcpyDeviceToHost));
+    return PPG_OK;
+}
+
+int ppg_pairs_emit_stats(const ppg_pairs *p, double *vals, int32_t n) {
+    if (!p || !vals || n < 0) return PPG_ARG_ERROR;
+    const PairEmit &E = p->em;
+    const double v[8] = {E.t_ms[0], E.t_ms[1], E.t_ms[2], E.t_ms[3], (double)E.reruns, (double)E.npc, (double)E.j_lo,
+                         (double)E.j_hi};
+    for (int32_t i = 0; i < n && i < 8; i++) vals[i] = v[i];
     return PPG_OK;
 }
 

@@ -474,8 +474,11 @@ extern "C" __global__ __launch_bounds__(256) void ppg_copy16(const uint4 *__rest
 // past every chunk's own -- are concatenated into the chunk's region, so the parse kernels see the
 // chunk as one job.  A chunk decoded whole censused straight into its region.  One block per chunk.
 // ------------------------------------------------------------------------------------------
+// inv (may be null): sub-job j's result is sres[inv[j]] -- the launch ran the sub-jobs in another
+// order (longest first, ppg_shard_set_split)
 extern "C" __global__ __launch_bounds__(256) void ppg_split_merge(const PpgInflateJob *__restrict__ sjobs,
                                                                   const PpgInflateResult *__restrict__ sres,
+                                                                  const uint32_t *__restrict__ inv,
                                                                   const uint32_t *__restrict__ sidx,
                                                                   const uint32_t *__restrict__ snls,
                                                                   const PpgInflateJob *__restrict__ jobs,
@@ -485,14 +488,14 @@ extern "C" __global__ __launch_bounds__(256) void ppg_split_merge(const PpgInfla
     if (k >= n) return;
     const uint32_t s0 = sidx[k], s1 = sidx[k + 1];
     if (s1 == s0 + 1) {   // decoded whole: its census is already in the chunk's region
-        if (threadIdx.x == 0) res[k] = sres[s0];
+        if (threadIdx.x == 0) res[k] = sres[inv ? inv[s0] : s0];
         return;
     }
     const PpgInflateJob &C = jobs[k];
     PpgInflateResult m = {};
     uint32_t nl = 0;
     for (uint32_t j = s0; j < s1; j++) {
-        const PpgInflateResult r = sres[j];
+        const PpgInflateResult r = sres[inv ? inv[j] : j];
         const bool tail = j + 1 == s1;
         if (m.status == 0 && r.status != 0) m.status = r.status;
         if (m.status == 0 && !tail && (r.produced != sjobs[j].out_len || r.end_bit != sjobs[j + 1].bit_start))
@@ -589,9 +592,9 @@ hipError_t ppg_launch_copy16(hipStream_t s, const void *src, void *dst, uint64_t
 }
 
 hipError_t ppg_launch_split_merge(hipStream_t s, const PpgInflateJob *sjobs, const PpgInflateResult *sres,
-                                  const uint32_t *sidx, const uint32_t *snls, const PpgInflateJob *jobs,
-                                  PpgInflateResult *res, uint32_t *nls, int n) {
+                                  const uint32_t *inv, const uint32_t *sidx, const uint32_t *snls,
+                                  const PpgInflateJob *jobs, PpgInflateResult *res, uint32_t *nls, int n) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_split_merge, dim3(n), dim3(256), 0, s, sjobs, sres, sidx, snls, jobs, res, nls, n);
+    hipLaunchKernelGGL(ppg_split_merge, dim3(n), dim3(256), 0, s, sjobs, sres, inv, sidx, snls, jobs, res, nls, n);
     return hipGetLastError();
 }

@@ -83,6 +83,46 @@ class Pairs:
         check(lib.ppg_pairs_records(self._h, int(f), int(lo), int(hi), C.c_void_p(out.ctypes.data)), "ppg_pairs_records")
         return out[:hi - lo]
 
+    # ---- record-aligned pair chunks (ppg_pairs_emit_*) ----
+    def emit(self, r1, r2, pair_chunk, comm=None, window_bytes=0):
+        """Yield windows (j0, j1) of this rank's record-aligned pair chunks [j0, j1) of `pair_chunk`
+        pairs, packed on the device (ppg_pairs_emit_begin / _next).  After check() on the same
+        shards and comm; a window's halves are read with chunk() / copy_chunk() before the next one
+        is made.  N ranks: every rank iterates (the first window is collective)."""
+        check(lib.ppg_pairs_emit_begin(self._h, r1.handle, r2.handle, comm.handle if comm is not None else None,
+                                       int(pair_chunk), int(window_bytes)), "ppg_pairs_emit_begin")
+        j0, j1 = C.c_int64(), C.c_int64()
+        while True:
+            rc = lib.ppg_pairs_emit_next(self._h, C.byref(j0), C.byref(j1))
+            if rc == 1:   # PPG_STREAM_END
+                return
+            check(rc, "ppg_pairs_emit_next")
+            yield j0.value, j1.value
+
+    def chunk(self, j, f):
+        """(device address of the bytes, length, device address of the descriptors, records) of
+        file f's half of pair chunk j (current window)."""
+        b, d, n, r = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int64()
+        check(lib.ppg_pairs_chunk(self._h, int(j), int(f), C.byref(b), C.byref(n), C.byref(d), C.byref(r)),
+              "ppg_pairs_chunk")
+        return b.value, n.value, d.value, r.value
+
+    def copy_chunk(self, j, f):
+        """(bytes, (n,4) uint32 descriptors) of file f's half of pair chunk j, in host memory."""
+        _, n, _, r = self.chunk(j, f)
+        buf = np.empty(max(1, n), np.uint8)
+        desc = np.empty((max(1, r), 4), np.uint32)
+        ln, nr = C.c_int64(), C.c_int64()
+        check(lib.ppg_pairs_copy_chunk(self._h, int(j), int(f), C.c_void_p(buf.ctypes.data), buf.size, C.byref(ln),
+                                       C.c_void_p(desc.ctypes.data), desc.shape[0], C.byref(nr)), "ppg_pairs_copy_chunk")
+        return buf[:n], desc[:r]
+
+    def emit_stats(self):
+        v = (C.c_double * 8)()
+        check(lib.ppg_pairs_emit_stats(self._h, v, 8), "ppg_pairs_emit_stats")
+        return {"rerun_ms": v[0], "pack_ms": v[1], "exchange_ms": v[2], "emit_ms": v[3], "reruns": int(v[4]),
+                "pair_chunks": int(v[5]), "mine": (int(v[6]), int(v[7]))}
+
     def close(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
@@ -115,19 +155,26 @@ def _read_range(path, index):
 class PairedFASTQ:
     """Two BatchedFASTQ streams zipped into record-aligned pair chunks of `pair_chunk` records
     (default 50,000, BASELINE configs[4]).  Both files are decoded on one GPU and their pairing
-    is verified on the device (ppg_pairs_check) before any pair is handed out."""
+    is verified on the device (ppg_pairs_check) before any pair is handed out; the pair chunks
+    themselves are packed on the device by the library (ppg_pairs_emit_*) window by window, and
+    each half is one copy out (FastqRecords over its bytes and descriptors)."""
 
-    def __init__(self, index1, gz1, index2, gz2, pair_chunk=50_000, device=None):
+    def __init__(self, index1, gz1, index2, gz2, pair_chunk=50_000, device=None, out_capacity=0,
+                 window_bytes=0):
         self.index = [IndexIO.Deserialize(i) if isinstance(i, str) else i for i in (index1, index2)]
         self.paths = [gz1, gz2]
         self.K = int(pair_chunk)
         self.dev = device or Device.default()
-        self.shards = [Shard(ix, _read_range(p, ix), 0, ix.Count - 1, device=self.dev).run()
-                       for ix, p in zip(self.index, self.paths)]
+        self.shards = []
+        for ix, p in zip(self.index, self.paths):
+            sh = Shard(ix, _read_range(p, ix), 0, ix.Count - 1, device=self.dev, out_capacity=out_capacity)
+            if sh.batches > 1:   # the spot keys per batch while resident (ppg_shard_set_keys)
+                attach_keys(sh, int(ix.point_fields(ix.Count - 1)[0]) // 32 + 4096)
+            self.shards.append(sh.run())
         self._pairs = Pairs()
         self.result = self._pairs.check(self.shards[0], self.shards[1])
         self.pairs = require_pairs(self.result)
-        self._bases = [np.asarray(s.record_base(), np.int64) for s in self.shards]
+        self.window_bytes = window_bytes
 
     def Count(self):
         return self.pairs
@@ -136,26 +183,21 @@ class PairedFASTQ:
     def chunks(self):
         return (self.pairs + self.K - 1) // self.K
 
-    def _records(self, f, lo, hi):
-        """FastqRecords of file f for pair numbers [lo, hi)."""
-        sh, ix, bases = self.shards[f], self.index[f], self._bases[f]
-        out, cache = [], {}
-        for r in self._pairs.records(f, lo, hi):   # shard record number of each pair
-            k = int(np.searchsorted(bases, r, side="right") - 1)
-            if k not in cache:
-                raw = bytes(ix[k].offset) + sh.chunk_bytes(k).tobytes()
-                cache = {k: records_from_descriptors(raw, sh.chunk_records(k))}
-            out.append(cache[k][int(r - bases[k])])
-        return out
+    def pair_chunks(self):
+        """Yield (j, R1 records, R2 records) for every pair chunk in order."""
+        for j0, j1 in self._pairs.emit(self.shards[0], self.shards[1], self.K, window_bytes=self.window_bytes):
+            for j in range(j0, j1):
+                yield (j,) + tuple(records_from_descriptors(*self._pairs.copy_chunk(j, f)) for f in (0, 1))
 
     def pair_chunk(self, j):
         """(R1 records, R2 records) of pair chunk j: pairs [j*K, min((j+1)*K, Count))."""
-        lo, hi = j * self.K, min((j + 1) * self.K, self.pairs)
-        if not 0 <= lo < hi:
+        if not 0 <= j < self.chunks:
             raise IndexError(j)
-        return self._records(0, lo, hi), self._records(1, lo, hi)
+        for jj, a, b in self.pair_chunks():
+            if jj == j:
+                return a, b
+        raise IndexError(j)
 
     def __iter__(self):
-        for j in range(self.chunks):
-            a, b = self.pair_chunk(j)
+        for _, a, b in self.pair_chunks():
             yield from zip(a, b)

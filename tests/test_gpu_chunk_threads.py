@@ -208,3 +208,45 @@ def test_bad_requests_fail_alone(file200k):
     # a corrupted deflate stream: zlib's verdict for these bytes (DATA_ERROR, or garbage that
     # still decodes) -- never a device error, never another request's failure
     assert set(outcomes["corrupt"]) <= {0, _lib.PPG_DATA_ERROR, _lib.PPG_BUF_ERROR}
+
+
+def test_async_submit_vs_oracle(file200k):
+    """ppg_decompress_chunk_submit / _wait from ONE caller thread (the
+    reference keeps 32 partitions queued, LazyFileReader.cs:14): every chunk of the 200k-record
+    member queued twice before any wait, the launcher thread combines them into few launches, every
+    result equals the oracle's; a bad request among them fails alone."""
+    gz, exp = file200k
+    dev = pp.Device(0)
+    ix = pp.Core.BuildDeflateIndex(gz, 2000)
+    n = ix.Count - 1
+    before = dev.decompress_chunk_stats()
+    futs = [(k, pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, k), ix, k, device=dev)) for k in list(range(n)) * 2]
+    bad = pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, 3)[:-1], ix, 3, device=dev)   # short slice
+    for k, f in futs:
+        got, buf, rec = f.result()
+        assert sha(buf[:got]) == exp[k][0], k
+        assert np.array_equal(rec, exp[k][1]), k
+    with pytest.raises(pp.PpgError) as e:
+        bad.result()
+    assert e.value.code == _lib.PPG_ARG_ERROR
+    st = dev.decompress_chunk_stats()
+    calls, launches = st["calls"] - before["calls"], st["launches"] - before["launches"]
+    assert calls == 2 * n + 1 and launches <= 8, (calls, launches, st)
+
+
+def test_async_and_threads_together(file200k):
+    """Asynchronous requests queued beside 8 synchronous caller threads on one ctx: all served, all
+    equal to the oracle's."""
+    gz, exp = file200k
+    dev = pp.Device(0)
+    ix = pp.Core.BuildDeflateIndex(gz, 2000)
+    n = ix.Count - 1
+    futs = [(k, pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, k), ix, k, device=dev)) for k in range(0, n, 2)]
+
+    def check(k, b, rec):
+        assert sha(b) == exp[k][0], k
+        assert np.array_equal(rec, exp[k][1]), k
+    chunk_calls(gz, ix, dev, list(range(1, n, 2)), check)
+    for k, f in futs:
+        got, buf, rec = f.result()
+        check(k, buf[:got], rec)

@@ -98,3 +98,49 @@ def test_configs4_full_size_pair_on_one_gpu(device):
     k = [paired.shard_keys(sh) for sh in shards]
     k = [x[x != paired.DUP] for x in k]
     assert torch.equal(k[0], k[1]) and bool((k[0] >= 0).all())
+    # record-aligned pair chunks at configs[4]'s K = 50,000 (the deliverable): every
+    # window packed on the device -- the shards' 40 GiB batches run again as the windows advance and
+    # pair chunks straddling a batch boundary carried -- every pair chunk once, K pairs each (the
+    # last fewer), the halves' bytes adding up to each member's text; the first pair chunk of every
+    # window (a carried one after each batch change) and the last compared byte for byte with the text
+    K = 50_000
+    pairs = 2_621_440 * reps
+    pr = paired.Pairs()
+    pr.check(shards[0], shards[1])
+    nbytes, nxt, windows = [0, 0], 0, 0
+    for j0, j1 in pr.emit(shards[0], shards[1], K, window_bytes=8 << 30):
+        assert j0 == nxt
+        for j in range(j0, j1):
+            for f in (0, 1):
+                _, n, _, r = pr.chunk(j, f)
+                assert r == min(K, pairs - j * K), (j, f, r)
+                nbytes[f] += n
+            if j == j0 or j == -(-pairs // K) - 1:
+                for f, tf in enumerate(tfs):
+                    b, d = pr.copy_chunk(j, f)
+                    eb = _records_text(tf, j * K, min((j + 1) * K, pairs))
+                    assert b.tobytes() == eb, (j, f)
+                    nl = np.nonzero(np.frombuffer(eb, np.uint8) == 10)[0].astype(np.uint32).reshape(-1, 4)
+                    assert np.array_equal(d, nl), (j, f)
+        nxt = j1
+        windows += 1
+    assert nxt == -(-pairs // K) and windows > 10
+    assert nbytes == [int(tf.p_output[-1]) for tf in tfs]
+    assert pr.emit_stats()["reruns"] >= shards[0].batches + shards[1].batches
+
+
+_STARTS = {}
+
+
+def _records_text(tf, lo, hi):
+    """Bytes of records [lo, hi) of a tiled member: its segment's records, repeated."""
+    if id(tf) not in _STARTS:
+        nl = np.nonzero(tf.text == 10)[0]
+        _STARTS[id(tf)] = np.concatenate([[0], nl[3::4] + 1]).astype(np.int64)
+    st, n, out, i = _STARTS[id(tf)], tf.records, [], lo
+    while i < hi:
+        r = i % n
+        take = min(hi - i, n - r)
+        out.append(tf.text[int(st[r]):int(st[r + take])].tobytes())
+        i += take
+    return b"".join(out)

@@ -6,7 +6,9 @@
 # Every step runs under its own time limit, writes under gpurun_out/<tag>/, and the first failing
 # step ends the call (a GPU fault, abort or time limit is never followed by more GPU work).
 # Steps:
-#   gputest[:<pytest -k expr>]  pytest -m gpu (all, or the -k selection)          -> gputest.txt
+# A step may carry arguments after ':' -- for gputest a -k selection with ',' for " or ", for the
+# bench steps extra bench.py arguments with '_' for a space (e.g. stamps:--share_8).
+#   gputest[:<k1,k2,...>]       pytest -m gpu (all, or the tests matching any k)   -> gputest.txt
 #   smoke                       __graft_entry__.smoke()                            -> smoke.txt
 #   bench                       the default bench line (python bench.py)           -> bench_default.json
 #   profile                     rocprofv3 kernel stats + FETCH/WRITE passes, summarised into
@@ -19,8 +21,8 @@
 #   shares                      N = 1 and rank 0's share of N = $SHARES (default "2 4 8"); variants
 #                               $VARIANTS = "tag:args" items ('_' = space)         -> shares/*.json
 #   ab                          tools/ab_multi.py over $AB_BUILDS ("tag=lib ...")   -> ab.json
-#   stamps                      the PPG_STAMPS diagnostic build (abtmp/stamps) on the bench workload,
-#                               $STAMP_ARGS appended (e.g. --share 8)              -> stamps.log
+#   stamps[:args]               the PPG_STAMPS diagnostic build (abtmp/stamps) on the bench workload
+#                               (e.g. stamps:--share_8)                            -> stamps*.log
 #   chunkapi                    the per-chunk Decompress leg only ($CHUNK_ARGS)    -> chunkapi.json
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -33,11 +35,12 @@ line() {   # the bench line's headline numbers
   python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; print(sys.argv[1], round(d['value']/1e6,2), d.get('unit'), round(d['ms_per_step'],2), 'ms', d.get('kernel_ms_per_step'), (d.get('roofline') or {}).get('frac'))" "$1"
 }
 run_step() {
-  local step=$1 arg=${1#*:}
+  local step=$1 arg=${1#*:} xa
   [ "$arg" = "$step" ] && arg=""
+  xa=${arg//_/ }
   case ${step%%:*} in
   gputest)
-    if [ -n "$arg" ]; then sel=(-k "$arg"); else sel=(); fi
+    if [ -n "$arg" ]; then sel=(-k "${arg//,/ or }"); else sel=(); fi
     timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread "${sel[@]}" > $O/gputest.txt 2>&1
     rc=$?; tail -2 $O/gputest.txt
     [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/gputest.txt | head -20; return $rc; } ;;
@@ -45,7 +48,7 @@ run_step() {
     timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail -5 $O/smoke.txt; return 1; }
     tail -1 $O/smoke.txt ;;
   bench)
-    timeout -k 10 500 python3 -u bench.py $BENCH_ARGS > $O/bench_default.json 2> $O/bench_default.log || return $?
+    timeout -k 10 500 python3 -u bench.py $xa > $O/bench_default.json 2> $O/bench_default.log || return $?
     line $O/bench_default.json ;;
   profile)
     bash tools/profile_round.sh || return $?
@@ -65,7 +68,7 @@ run_step() {
     line $O/paired.json ;;
   w8)
     PPG_BENCH_ONE_DEVICE=1 PPG_DIST_BACKEND=gloo timeout -k 10 900 python3 -u bench.py --gpus 8 --steps 2 --warmup 1 \
-      $NOLEGS $W8_ARGS > $O/w8.json 2> $O/w8.log || { tail -20 $O/w8.log; return 1; }
+      $NOLEGS $W8_ARGS $xa > $O/w8.json 2> $O/w8.log || { tail -20 $O/w8.log; return 1; }
     line $O/w8.json ;;
   shares)
     mkdir -p $O/shares
@@ -87,11 +90,12 @@ run_step() {
     tail -c 1500 $O/ab.json ;;
   stamps)
     [ -f abtmp/stamps/ppg_inflate.lint ] || { echo "stamps: build abtmp/stamps first (tools/ab_build.sh stamps -DPPG_STAMPS)"; return 3; }
-    PPG_LIB_PATH=abtmp/stamps/libppgpu.so timeout -k 10 300 python3 -u bench.py --steps 1 --warmup 1 $NOLEGS $STAMP_ARGS \
-      > $O/stamps$STAMP_TAG.json 2> $O/stamps$STAMP_TAG.log || return $?
-    grep PPG_STAMPS $O/stamps$STAMP_TAG.log | tail -4 ;;
+    local st=stamps${arg:+_${arg//[^a-z0-9]/}}
+    PPG_LIB_PATH=abtmp/stamps/libppgpu.so timeout -k 10 300 python3 -u bench.py --steps 1 --warmup 1 $NOLEGS $xa \
+      > $O/$st.json 2> $O/$st.log || return $?
+    grep PPG_STAMPS $O/$st.log | tail -4 ;;
   chunkapi)
-    timeout -k 10 400 python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-enumerate $CHUNK_ARGS \
+    timeout -k 10 400 python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-enumerate $xa \
       > $O/chunkapi.json 2> $O/chunkapi.log || return $?
     python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); c=d.get('decompress_chunk', {}); print(json.dumps(c)[:1500])" $O/chunkapi.json ;;
   *)
