@@ -39,6 +39,9 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n, const uint32_t *nls);
+hipError_t ppg_launch_materialize(hipStream_t s, const uint16_t *sym, const uint8_t *wins, const PpgMatInfo *mi,
+                                  const PpgInflateJob *jobs, uint8_t *out, PpgInflateResult *res, int njobs,
+                                  uint32_t *nls);
 hipError_t ppg_launch_split_merge(hipStream_t s, const PpgInflateJob *sjobs, const PpgInflateResult *sres,
                                   const uint32_t *inv, const uint32_t *sidx, const uint32_t *snls,
                                   const PpgInflateJob *jobs, PpgInflateResult *res, uint32_t *nls, int n);
@@ -655,7 +658,15 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     hipStream_t s = shard_stream(sh);
     const int nb = b1 - b0;
     HIPCHK(hipEventRecord(sh->ev[0], s));
-    if (sh->nsub) {   // the batch's sub-jobs (longest first, see ppg_shard_set_split), then one result per chunk
+    if (sh->nsub && sh->mat_n) {   // one batch: sub-jobs [0, mat_first) decoded, the rest materialised
+        const uint32_t ns = sh->h_sidx[(size_t)sh->n];
+        HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
+                                  sh->ljobs.p, sh->dicts.p, sh->out.p, sh->sres.p, (int)sh->mat_first, sh->nls.p));
+        HIPCHK(ppg_launch_materialize(s, sh->mat_sym, sh->mat_win, sh->mat_info, sh->ljobs.p + sh->mat_first, sh->out.p,
+                                      sh->sres.p + sh->mat_first, (int)(ns - sh->mat_first), sh->nls.p));
+        HIPCHK(ppg_launch_split_merge(s, sh->sjobs.p, sh->sres.p, sh->linv.p, sh->sidx.p + b0, sh->nls.p,
+                                      sh->jobs.p + b0, sh->res.p + b0, sh->nls.p, nb));
+    } else if (sh->nsub) {   // the batch's sub-jobs (longest first, see ppg_shard_set_split), then one result per chunk
         const uint32_t s0 = sh->h_sidx[(size_t)b0], s1 = sh->h_sidx[(size_t)b1];
         const bool lpt = sh->lpt;
         HIPCHK(ppg_launch_inflate(s, sh->ctx->ring_bits, sh->ctx->lit_bits, (const uint32_t *)sh->comp, sh->nwords,
@@ -779,6 +790,16 @@ int ppg_shard_run(ppg_shard *sh) {
 int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
                         const uint8_t *windows) {
     if (!sh || nsub < 0 || (nsub && (!bit || !output || !windows))) return PPG_ARG_ERROR;
+    return shard_set_split_impl(sh, nsub, bit, output, windows, true);
+}
+
+}  // extern "C"
+
+// windows == nullptr: the pieces are not decoded from their side points (the lone-chunk Decompress
+// materialises them from its pass-1 symbols, ppg_chunk.cpp): no dictionaries, no prev_byte; lpt =
+// false: the caller sets the launch order (ljobs / linv) itself
+int shard_set_split_impl(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
+                         const uint8_t *windows, bool lpt) {
     HIPCHK(hipSetDevice(sh->ctx->device));
     hipStream_t s = shard_stream(sh);
     const int32_t n = sh->n;
@@ -839,7 +860,7 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
                 J.bit_start = (uint64_t)(bit[q] - 8 * base_byte);
                 J.dict_off = ((uint64_t)n + (uint64_t)q) * kWin;
                 J.raw_shift = C.raw_shift + (uint32_t)lo;
-                J.prev_byte = windows[(size_t)q * kWin + kWin - 1];
+                J.prev_byte = windows ? windows[(size_t)q * kWin + kWin - 1] : 0u;
             }
             const int64_t hi = j + 1 < hidx[(size_t)k + 1] ? output[t] - from_out : (int64_t)C.out_len;
             J.out_off = C.out_off + (uint64_t)lo;
@@ -856,13 +877,14 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     // dictionaries: the chunks' windows, then the side points' (in place when shard_reserve or an
     // earlier split left room)
     DevBuf<uint8_t> d2;
-    if (sh->dicts.n < ((size_t)n + (size_t)nsub) * kWin) {
+    if (windows && sh->dicts.n < ((size_t)n + (size_t)nsub) * kWin) {
         HIPCHK(d2.alloc(((size_t)n + (size_t)nsub) * kWin));
         HIPCHK(hipMemcpyAsync(d2.p, sh->dicts.p, (size_t)n * kWin, hipMemcpyDeviceToDevice, s));
         std::swap(sh->dicts.p, d2.p);
         std::swap(sh->dicts.n, d2.n);
     }
-    HIPCHK(hipMemcpyAsync(sh->dicts.p + (size_t)n * kWin, windows, (size_t)nsub * kWin, hipMemcpyHostToDevice, s));
+    if (windows)
+        HIPCHK(hipMemcpyAsync(sh->dicts.p + (size_t)n * kWin, windows, (size_t)nsub * kWin, hipMemcpyHostToDevice, s));
     HIPCHK(sh->sjobs.alloc(sh->h_sjobs.size()));
     HIPCHK(hipMemcpyAsync(sh->sjobs.p, sh->h_sjobs.data(), sizeof(PpgInflateJob) * sh->h_sjobs.size(),
                           hipMemcpyHostToDevice, s));
@@ -879,7 +901,8 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     // in launch order and ppg_split_merge reads them through the inverse permutation.
     // PPG_SPLIT_ORDER=0: the sub-jobs in chunk order.
     static const bool lpt_off = [] { const char *e = getenv("PPG_SPLIT_ORDER"); return e && *e == '0'; }();
-    sh->lpt = !lpt_off;
+    sh->lpt = lpt && !lpt_off;
+    sh->mat_n = 0;
     if (sh->lpt) {
         const size_t ns = sh->h_sjobs.size();
         std::vector<uint32_t> perm(ns), inv(ns);
@@ -905,6 +928,8 @@ int ppg_shard_set_split(ppg_shard *sh, int32_t nsub, const int64_t *bit, const i
     sh->nsub = nsub;
     return PPG_OK;
 }
+
+extern "C" {
 
 int ppg_shard_results(ppg_shard *sh, int64_t *records, int64_t *produced, int32_t *status, int32_t *flags,
                       int64_t *end_bit) {

@@ -26,10 +26,13 @@
 #include <thread>
 
 hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
-                                 const uint64_t *hi, uint64_t *cand, int n);
+                                 const uint64_t *hi, uint64_t *cand, int n, int sub);
 hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs);
+hipError_t ppg_launch_inflate_ixf(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
+                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
+                                  int njobs);
 hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
                              const uint8_t *ref, uint32_t *diff, int n);
 hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
@@ -78,8 +81,16 @@ hipError_t grow_buf(B &b, size_t need) {
     return b.alloc(std::max(need, b.n + b.n / 2));
 }
 
+// waves per candidate range of the block search: enough for ~4,096 waves in all (a lone chunk's 16
+// ranges are searched by 16 waves each; a launch of hundreds of chunks fills the GPU with one each)
+int find_sub(int ranges) { return std::max(1, std::min(32, 4096 / std::max(1, ranges))); }
+
 // device scratch of find_side_points (grow only)
 struct FindScratch {
+    DevBuf<uint16_t> sym;                  // materialise path: every piece's pass-1 symbols, whole
+    DevBuf<PpgMatInfo> mi;
+    DevBuf<PpgInflateJob> lj;              // its launch order
+    DevBuf<uint32_t> linv;
     DevBuf<uint64_t> lo, hi, cand;
     DevBuf<PpgInflateJob> jobs;
     DevBuf<PpgInflateResult> res;
@@ -239,7 +250,7 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
     HIPCHK(grow_buf(F.cand, nc));
     HIPCHK(hipMemcpyAsync(F.lo.p, lo.data(), 8 * nc, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(F.hi.p, hi.data(), 8 * nc, hipMemcpyHostToDevice, s));
-    HIPCHK(ppg_launch_block_find(s, comp, nwords, F.lo.p, F.hi.p, F.cand.p, (int)nc));
+    HIPCHK(ppg_launch_block_find(s, comp, nwords, F.lo.p, F.hi.p, F.cand.p, (int)nc, find_sub((int)nc)));
     std::vector<uint64_t> cand(nc);
     HIPCHK(hipMemcpyAsync(cand.data(), F.cand.p, 8 * nc, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -375,6 +386,201 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
     return PPG_OK;
 }
 
+// ---- the materialise path: one symbolic decode per piece instead of two (r05) ----
+// A launch of at most kMatMaxChunks chunks of plain indexes (no side points of their own) splits
+// each chunk at the inner block starts found on the GPU as find_side_points does, but its pass 1
+// covers the WHOLE chunk -- the last piece too, up to the chunk's end -- and keeps every piece's
+// symbolic output whole (ppg_inflate_kernel IXF).  A chunk whose chain of block ends is verified
+// from its Point to its end gets its pieces' exact starting histories resolved from the symbolic
+// tails and is then written out from the symbols (ppg_materialize_kernel, with the fused newline
+// census) -- no second decode; any other chunk is decoded whole, one wave, in the same launch.
+// A lone 10,000-record chunk: find ~0.5 ms + one symbolic decode of a single deflate block (~4 ms)
+// + resolve + materialise, instead of that plus a second decode of the same block.
+constexpr int kMatMaxChunks = 256;
+constexpr uint64_t kMatRatio = 10;        // symbol capacity per compressed byte of a piece (FASTQ: ~4)
+
+struct MatPiece {
+    uint64_t start, stop;       // bits: piece start, the next piece's start (the chunk's end for the last)
+    uint64_t sym_off, cap;      // symbols
+};
+
+int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const std::vector<FindChunk> &ch,
+             std::vector<uint8_t> &covered, std::vector<std::vector<PpgMatInfo>> &pmi,
+             std::vector<std::vector<int64_t>> &pbit, std::vector<std::vector<int64_t>> &pout, PhaseClock &clk) {
+    hipStream_t s = sl.s;
+    FindScratch &F = sl.fs;
+    covered.assign(ch.size(), 0);
+    pmi.assign(ch.size(), {});
+    pbit.assign(ch.size(), {});
+    pout.assign(ch.size(), {});
+    std::vector<uint64_t> lo, hi;
+    std::vector<size_t> cfirst(ch.size() + 1, 0);
+    for (size_t c = 0; c < ch.size(); c++) {
+        const uint64_t span = ch[c].bit1 - ch[c].bit0;
+        const uint64_t pb = std::max<uint64_t>(8ull * 48 * 1024, span / 16);
+        for (uint64_t a = ch[c].bit0 + pb; a + 8ull * 1024 < ch[c].bit1; a += pb) {
+            lo.push_back(a);
+            hi.push_back(std::min(a + pb, ch[c].bit1));
+        }
+        cfirst[c + 1] = lo.size();
+    }
+    const size_t nc = lo.size();
+    std::vector<uint64_t> cand(nc);
+    if (nc) {
+        HIPCHK(grow_buf(F.lo, nc));
+        HIPCHK(grow_buf(F.hi, nc));
+        HIPCHK(grow_buf(F.cand, nc));
+        HIPCHK(hipMemcpyAsync(F.lo.p, lo.data(), 8 * nc, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(F.hi.p, hi.data(), 8 * nc, hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_block_find(s, comp, nwords, F.lo.p, F.hi.p, F.cand.p, (int)nc, find_sub((int)nc)));
+        HIPCHK(hipMemcpyAsync(cand.data(), F.cand.p, 8 * nc, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    clk.mark("f.cand");
+    // pieces: the Point, the candidates, up to the chunk's end; symbol capacity by compressed size
+    std::vector<MatPiece> pc;
+    std::vector<size_t> pfirst(ch.size() + 1, 0);
+    uint64_t syms = 0;
+    for (size_t c = 0; c < ch.size(); c++) {
+        std::vector<uint64_t> st{ch[c].bit0};
+        for (size_t k = cfirst[c]; k < cfirst[c + 1]; k++)
+            if (cand[k] != ~0ull && cand[k] > st.back() && cand[k] < ch[c].bit_end) st.push_back(cand[k]);
+        st.push_back(ch[c].bit_end);
+        for (size_t j = 0; j + 1 < st.size(); j++) {
+            const uint64_t cap = std::max<uint64_t>(64 * 1024, kMatRatio * ((st[j + 1] - st[j]) / 8 + 64));
+            pc.push_back(MatPiece{st[j], st[j + 1], syms, cap});
+            syms += cap + 2048;   // flushes may run up to a unit past the capacity check
+        }
+        pfirst[c + 1] = pc.size();
+    }
+    const size_t np = pc.size();
+    if (!np) return PPG_OK;
+    std::vector<PpgInflateJob> jobs(np);
+    uint64_t nblk = 0;
+    for (size_t q = 0; q < np; q++) {
+        PpgInflateJob &J = jobs[q];
+        J = PpgInflateJob{};
+        J.bit_start = pc[q].start;
+        J.bit_limit = std::max<uint64_t>(pc[q].stop, 0);
+        J.out_off = pc[q].sym_off;
+        J.out_len = pc[q].cap;
+        J.expect_end = ~0ull;
+        J.stop_bit = pc[q].stop;
+        J.blk_off = (uint32_t)nblk;
+        J.blk_cap = (uint32_t)((pc[q].stop - pc[q].start) / 8 / 2048 + 64);
+        nblk += J.blk_cap;
+    }
+    // the piece may read up to its chunk's slice end (the last block of a non-final piece ends past
+    // its stop when the next candidate was false)
+    for (size_t c = 0; c < ch.size(); c++)
+        for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) jobs[q].bit_limit = ch[c].bit1;
+    HIPCHK(grow_buf(F.jobs, np));
+    HIPCHK(grow_buf(F.res, np));
+    HIPCHK(grow_buf(F.blk, (size_t)nblk));
+    HIPCHK(grow_buf(F.sym, (size_t)syms + 64));
+    HIPCHK(grow_buf(F.ta, np * 2 * kWin));
+    if (!F.ident.p) {   // u16 0..32767: position p < 0 of a piece is history symbol 32768 + p
+        std::vector<uint16_t> id(kWin);
+        for (int i = 0; i < kWin; i++) id[(size_t)i] = (uint16_t)i;
+        HIPCHK(F.ident.alloc(2 * kWin));
+        HIPCHK(hipMemcpyAsync(F.ident.p, id.data(), 2 * kWin, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemcpyAsync(F.jobs.p, jobs.data(), sizeof(PpgInflateJob) * np, hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_inflate_ixf(s, comp, nwords, F.jobs.p, F.ident.p, (uint8_t *)F.sym.p, F.res.p, F.blk.p, (int)np));
+    std::vector<PpgInflateResult> res(np);
+    std::vector<PpgBlockEnd> blk((size_t)nblk);
+    HIPCHK(hipMemcpyAsync(res.data(), F.res.p, sizeof(PpgInflateResult) * np, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(blk.data(), F.blk.p, sizeof(PpgBlockEnd) * nblk, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    clk.mark("f.pass1");
+    // a chunk is covered when its pieces chain from its Point to its end: every piece ends exactly
+    // where the next starts (its last block end), the last exactly at the chunk's end (or with the
+    // final block, for the file's last chunk), and their outputs add up to the chunk's
+    std::vector<size_t> wbase(ch.size(), 0);
+    std::vector<uint64_t> E(np, 0);
+    size_t nw = 0;
+    for (size_t c = 0; c < ch.size(); c++) {
+        bool ok = pfirst[c + 1] > pfirst[c];
+        uint64_t tot = 0;
+        for (size_t q = pfirst[c]; ok && q < pfirst[c + 1]; q++) {
+            const PpgInflateResult &r = res[q];
+            const uint32_t nb = std::min(r.nblocks, jobs[q].blk_cap);
+            if (r.status != 0 || nb == 0 || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN))) { ok = false; break; }
+            const PpgBlockEnd &e = blk[jobs[q].blk_off + nb - 1];
+            E[q] = e.end_bit;
+            if (e.out_end != r.produced) { ok = false; break; }
+            const bool lastp = q + 1 == pfirst[c + 1];
+            if (!lastp && (r.last || e.end_bit != pc[q].stop)) { ok = false; break; }
+            if (lastp && !(e.end_bit == ch[c].bit_end || (r.last && ch[c].bit_end == ch[c].bit1))) { ok = false; break; }
+            tot += r.produced;
+        }
+        ok = ok && (int64_t)tot == ch[c].len;
+        covered[c] = ok;
+        if (ok) {
+            wbase[c] = nw;
+            nw += pfirst[c + 1] - pfirst[c];
+        }
+    }
+    if (!nw) return PPG_OK;
+    // symbolic tails (the last 32 Ki symbols of each piece, as two 32 KiB byte halves), then every
+    // covered chunk's starting histories: W[0] = the Point's window, W[j+1] = T_j(W[j])
+    std::vector<PpgGather> g(2 * np);
+    for (size_t q = 0; q < np; q++) {
+        const uint64_t endb = 2 * res[q].produced, base = 2 * pc[q].sym_off;
+        g[2 * q] = PpgGather{base, (uint64_t)kWin, endb - kWin, ~0ull, 0};
+        g[2 * q + 1] = PpgGather{base, (uint64_t)kWin, endb, ~0ull, 0};
+    }
+    HIPCHK(grow_buf(F.gat, 2 * np));
+    HIPCHK(hipMemcpyAsync(F.gat.p, g.data(), sizeof(PpgGather) * 2 * np, hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_gather(s, (const uint8_t *)F.sym.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * np)));
+    size_t cmax = 0;
+    for (size_t c = 0; c < ch.size(); c++)
+        if (covered[c]) cmax = std::max(cmax, pfirst[c + 1] - pfirst[c]);
+    HIPCHK(grow_buf(F.W, nw * kWin));
+    HIPCHK(grow_buf(F.slots, nw));
+    HIPCHK(grow_buf(F.maps, (size_t)ppg_resolve_groups((int)cmax) * kWin));
+    std::vector<uint32_t> sl_all(nw, 0);
+    for (size_t c = 0; c < ch.size(); c++)
+        if (covered[c])
+            for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) sl_all[wbase[c] + (q - pfirst[c])] = (uint32_t)q;
+    HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * nw, hipMemcpyHostToDevice, s));
+    for (size_t c = 0; c < ch.size(); c++) {
+        if (!covered[c]) continue;
+        uint8_t *W = F.W.p + wbase[c] * kWin;
+        HIPCHK(hipMemcpyAsync(W, ch[c].window, kWin, hipMemcpyHostToDevice, s));
+        const size_t m = pfirst[c + 1] - pfirst[c];
+        if (m > 1) HIPCHK(ppg_launch_resolve(s, F.ta.p, nullptr, F.slots.p + wbase[c], (int)(m - 1), W, F.maps.p));
+    }
+    // the pieces' materialise info, side points at every later piece's start (launch coordinates)
+    for (size_t c = 0; c < ch.size(); c++) {
+        if (!covered[c]) continue;
+        uint64_t outc = 0, last_end = 0;
+        for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) {
+            const size_t j = q - pfirst[c];
+            last_end = E[q];
+            if (res[q].produced == 0) continue;   // an empty piece (a flush block) adds nothing
+            if (!pmi[c].empty()) {
+                pbit[c].push_back((int64_t)pc[q].start);
+                pout[c].push_back(ch[c].out0 + (int64_t)outc);
+            }
+            PpgMatInfo m{};
+            m.sym_off = pc[q].sym_off;
+            m.win_off = (wbase[c] + j) * (uint64_t)kWin;
+            m.nblocks = res[q].nblocks;
+            m.last = res[q].last;
+            m.prev = pmi[c].empty() ? 0x100u : 0x1FFu;   // 0x100: the chunk job's own (set below)
+            pmi[c].push_back(m);
+            outc += res[q].produced;
+        }
+        // each piece's end: where the next starts, the last one's block end
+        for (size_t i = 0; i < pmi[c].size(); i++)
+            pmi[c][i].end_bit = i + 1 < pmi[c].size() ? (uint64_t)pbit[c][i] : last_end;
+        if (pmi[c].empty()) covered[c] = 0;
+    }
+    clk.mark("f.resolve", s);
+    return PPG_OK;
+}
+
 // One launch of the requests `batch` on slot `sl` (the caller holds the slot, not the lock).  Sets
 // every request's rc and, for a decoded chunk, where its bytes and descriptors sit in sl.res.
 int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<ChunkReq *> &batch) {
@@ -447,7 +653,75 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     int rc = shard_prepare_specs(sh, spec.data(), (int32_t)go.size(), sl.comp.p, (int64_t)comp_len, 0, sl.s, nullptr);
     if (rc != PPG_OK) return rc;
     pc.mark("prepare");
-    {   // side points of the chunks that have them (the index's, shifted into this launch); the
+    bool mat = go.size() <= (size_t)kMatMaxChunks && !getenv("PPG_CHUNK_NO_FIND") && !getenv("PPG_CHUNK_NO_MAT");
+    for (size_t i = 0; mat && i < go.size(); i++) mat = go[i]->ix->side_out.empty();
+    if (mat) {   // the materialise path (find_mat above)
+        std::vector<FindChunk> find;
+        for (size_t i = 0; i < go.size(); i++) {
+            const PpgInflateJob &J = sh->h_jobs[i];
+            find.push_back(FindChunk{J.bit_start, J.bit_limit, J.expect_end != ~0ull ? J.expect_end : J.bit_limit,
+                                     sh->h_pout[i], (int64_t)J.out_len, go[i]->ix->win((size_t)go[i]->k)});
+        }
+        std::vector<uint8_t> covered;
+        std::vector<std::vector<PpgMatInfo>> pmi;
+        std::vector<std::vector<int64_t>> pbit, pout;
+        rc = find_mat(sl, (const uint32_t *)sl.comp.p, sh->nwords, find, covered, pmi, pbit, pout, pc);
+        if (rc != PPG_OK) return rc;
+        std::vector<int64_t> sbit, sout;
+        size_t ncov = 0;
+        for (size_t i = 0; i < go.size(); i++) {
+            if (!covered[i]) continue;
+            ncov++;
+            sbit.insert(sbit.end(), pbit[i].begin(), pbit[i].end());
+            sout.insert(sout.end(), pout[i].begin(), pout[i].end());
+        }
+        svc.found_chunks += (int64_t)ncov;
+        svc.found_points += (int64_t)sbit.size();
+        if (!sbit.empty()) {   // (chunks of one piece each only: decoded as usual)
+            rc = shard_set_split_impl(sh, (int32_t)sbit.size(), sbit.data(), sout.data(), nullptr, false);
+            if (rc != PPG_OK) return rc;
+            // launch order: the chunks decoded whole first (longest first), then the materialised pieces
+            const auto &X = sh->h_sidx;
+            const size_t ns = X[go.size()];
+            std::vector<uint32_t> order;
+            for (size_t i = 0; i < go.size(); i++)
+                if (!covered[i]) order.push_back(X[i]);
+            std::stable_sort(order.begin(), order.end(),
+                             [&](uint32_t a, uint32_t b) { return sh->h_sjobs[a].out_len > sh->h_sjobs[b].out_len; });
+            const uint32_t ndec = (uint32_t)order.size();
+            std::vector<PpgMatInfo> lmi;
+            for (size_t i = 0; i < go.size(); i++) {
+                if (!covered[i]) continue;
+                if (X[i + 1] - X[i] != pmi[i].size()) return PPG_DATA_ERROR;   // side points and pieces disagree
+                for (uint32_t j = X[i]; j < X[i + 1]; j++) {
+                    order.push_back(j);
+                    PpgMatInfo m = pmi[i][j - X[i]];
+                    if (m.prev == 0x100u) m.prev = sh->h_sjobs[j].prev_byte;   // the chunk's first piece
+                    lmi.push_back(m);
+                }
+            }
+            std::vector<PpgInflateJob> lj(ns);
+            std::vector<uint32_t> inv(ns);
+            for (size_t q = 0; q < ns; q++) {
+                lj[q] = sh->h_sjobs[order[q]];
+                inv[order[q]] = (uint32_t)q;
+            }
+            HIPCHK(sh->ljobs.alloc(ns));
+            HIPCHK(sh->linv.alloc(ns));
+            HIPCHK(grow_buf(sl.fs.mi, lmi.size()));
+            HIPCHK(hipMemcpyAsync(sh->ljobs.p, lj.data(), sizeof(PpgInflateJob) * ns, hipMemcpyHostToDevice, sl.s));
+            HIPCHK(hipMemcpyAsync(sh->linv.p, inv.data(), 4 * ns, hipMemcpyHostToDevice, sl.s));
+            HIPCHK(hipMemcpyAsync(sl.fs.mi.p, lmi.data(), sizeof(PpgMatInfo) * lmi.size(), hipMemcpyHostToDevice, sl.s));
+            sh->lpt = true;
+            sh->mat_first = ndec;
+            sh->mat_n = (uint32_t)lmi.size();
+            sh->mat_sym = sl.fs.sym.p;
+            sh->mat_win = sl.fs.W.p;
+            sh->mat_info = sl.fs.mi.p;
+            HIPCHK(hipStreamSynchronize(sl.s));   // the host staging vectors die here
+        }
+        pc.mark("split");
+    } else {   // side points of the chunks that have them (the index's, shifted into this launch); the
         // others' found on the GPU when the launch is too small to fill it
         std::vector<int64_t> sbit, sout;
         ByteVec swin;
@@ -481,8 +755,14 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     }
     shard_reset(sh);
     float total_ms = 0;
-    if ((rc = batch_launch(sh, 0, sh->n)) != PPG_OK) return rc;
-    if ((rc = batch_collect(sh, 0, sh->n, total_ms)) != PPG_OK) return rc;
+    rc = batch_launch(sh, 0, sh->n);
+    if (rc == PPG_OK) rc = batch_collect(sh, 0, sh->n, total_ms);
+    if (sh->mat_n) {   // the slot's shard is reused: the next launch sets its own split
+        sh->mat_n = 0;
+        sh->nsub = 0;
+        sh->lpt = false;
+    }
+    if (rc != PPG_OK) return rc;
     pc.mark("decode");
     // shard_finish returns the first chunk's zlib status (each request gets its own below) or a
     // device failure, which fails every request of the launch

@@ -54,6 +54,17 @@ struct PpgAtStats {
 };
 
 // offset_k bytes (Common/Index.cs:75) live concatenated in one device buffer
+// ppg_materialize_kernel: where a piece's pass-1 symbols and its exact starting history are
+struct PpgMatInfo {
+    uint64_t sym_off;     // first symbol (positions) in the pass-1 output buffer
+    uint64_t win_off;     // its 32 KiB starting history in the window buffer (bytes)
+    uint64_t end_bit;     // the piece's last block end (its result's end_bit)
+    uint32_t nblocks;
+    uint32_t last;        // the piece ends with the final block
+    uint32_t prev;        // the census's previous byte, or > 255: the history's last byte
+    uint32_t pad;
+};
+
 struct PpgOffsetRef {
     uint64_t start;
     uint32_t len;

@@ -196,6 +196,12 @@ struct ppg_shard {
     bool lpt = false;                           // the launch runs ljobs: sub-jobs longest first per batch,
     DevBuf<PpgInflateJob> ljobs;                // results in that order, sub-job j's at linv[j]
     DevBuf<uint32_t> linv;
+    // one-batch launches whose pieces are materialised from pass-1 symbols (ppg_chunk.cpp): ljobs
+    // [0, mat_first) are decoded, [mat_first, nsub + n) materialised with mat_info (launch order)
+    uint32_t mat_n = 0, mat_first = 0;
+    const uint16_t *mat_sym = nullptr;
+    const uint8_t *mat_win = nullptr;
+    const PpgMatInfo *mat_info = nullptr;
 };
 
 // one chunk of a shard: its Points, its window and where file byte from.Input-1 sits in comp
@@ -215,6 +221,8 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1);
 int batch_collect(ppg_shard *sh, int32_t b0, int32_t b1, float &total_ms);
 int shard_finish(ppg_shard *sh, float total_ms);
 int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, int32_t n);
+int shard_set_split_impl(ppg_shard *sh, int32_t nsub, const int64_t *bit, const int64_t *output,
+                         const uint8_t *windows, bool lpt);
 int shard_reserve(ppg_shard *sh, const ppg_index *ix, int32_t first,
                   const std::vector<std::pair<int32_t, int32_t>> &ranges, bool split);
 bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads);

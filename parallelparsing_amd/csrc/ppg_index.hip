@@ -12,6 +12,7 @@
 //   ppg_resolve_kernel      exact starting histories of all pieces from their symbolic tails
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 
@@ -60,6 +61,11 @@ __device__ bool header_ok(const uint32_t *comp, uint64_t nwords, uint64_t c, Fin
     if (build_table<CB>(S.lens, 19, S.cl, nullptr, S.sorted, TAB_CL, lane) != 0) return false;
     uint32_t idx = 0;
     const uint32_t total = hlit + hdist;
+    // running Kraft sums (units of 2^-15) of the litlen and distance codes: an over-subscribed code
+    // is one inflate_table refuses, so a false start -- random bits decode into code lengths that
+    // over-subscribe within a few symbols -- is rejected here instead of after all hlit + hdist
+    // lengths (r05: this check and the staged scan took a lone chunk's search 4.4 -> ~0.3 ms)
+    uint32_t kl = 0, kd = 0;
     while (idx < total) {
         const uint32_t e = uni(S.cl[g.peek() & ((1u << CB) - 1)]);
         const uint32_t L = e & 15;
@@ -79,6 +85,12 @@ __device__ bool header_ok(const uint32_t *comp, uint64_t nwords, uint64_t c, Fin
             rep = 11 + g.take(7);
         }
         if (idx + rep > total) return false;
+        if (val) {
+            const uint32_t nl = idx < hlit ? min(rep, hlit - idx) : 0u, nd = rep - nl;
+            kl += nl << (15 - val);
+            kd += nd << (15 - val);
+            if (kl > (1u << 15) || kd > (1u << 15)) return false;
+        }
         for (uint32_t j0 = 0; j0 < rep; j0 += 64)
             if (j0 + lane < rep) S.lens[idx + j0 + lane] = (uint8_t)val;
         idx += rep;
@@ -96,6 +108,9 @@ __device__ bool header_ok(const uint32_t *comp, uint64_t nwords, uint64_t c, Fin
 // cand[k] = the first bit b in [lo[k], hi[k]) where a dynamic Huffman block header zlib would
 // accept starts, or ~0.  Prefilter per lane: BFINAL = 0, BTYPE = 2, HLIT <= 29, HDIST <= 29 and a complete
 // code-length code (Kraft sum exactly 1); survivors get the full header_ok check, lowest first.
+// sub > 1: range k is searched by `sub` waves at once (blockIdx.y = part of the range), each from
+// the start of its part; the lowest find wins (atomic min; cand[k] = ~0 beforehand) -- a lone
+// chunk's few ranges then take a fraction of one wave's scan (ppg_decompress_chunk)
 __global__ __launch_bounds__(64) void ppg_block_find_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                             const uint64_t *__restrict__ lo,
                                                             const uint64_t *__restrict__ hi, uint64_t *cand, int n) {
@@ -103,7 +118,14 @@ __global__ __launch_bounds__(64) void ppg_block_find_kernel(const uint32_t *__re
     const int k = blockIdx.x;
     const int lane = threadIdx.x;
     if (k >= n) return;
-    const uint64_t a = lo[k], b = hi[k];
+    const uint32_t sub = gridDim.y, part = blockIdx.y;
+    uint64_t a = lo[k], b = hi[k];
+    if (sub > 1) {
+        const uint64_t span = b > a ? b - a : 0;
+        const uint64_t a2 = a + span * part / sub, b2 = a + span * (part + 1) / sub;
+        a = a2;
+        b = b2;
+    }
     uint64_t found = ~0ull;
     for (uint64_t base = a; base < b; base += 64) {
         const uint64_t bit = base + (uint64_t)lane;
@@ -138,8 +160,16 @@ __global__ __launch_bounds__(64) void ppg_block_find_kernel(const uint32_t *__re
             m &= m - 1;
         }
         if (found != ~0ull) break;
+        // a lower part has found one already: nothing here can win
+        if (sub > 1 && part > 0 && uni64(*(volatile const uint64_t *)&cand[k]) < a) break;
     }
-    if (lane == 0) cand[k] = found;
+    if (lane == 0) {
+        if (sub > 1) {
+            if (found != ~0ull) atomicMin((unsigned long long *)&cand[k], (unsigned long long)found);
+        } else {
+            cand[k] = found;
+        }
+    }
 }
 
 // dst[k] = the 32 KiB of history before output position g[k].end of a piece: position p >= 0 is
@@ -392,9 +422,14 @@ hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *t
 }
 
 hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
-                                 const uint64_t *hi, uint64_t *cand, int n) {
+                                 const uint64_t *hi, uint64_t *cand, int n, int sub) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_block_find_kernel, dim3(n), dim3(64), 0, s, comp, nwords, lo, hi, cand, n);
+    sub = std::max(1, std::min(sub, 256));
+    if (sub > 1) {
+        const hipError_t e = hipMemsetAsync(cand, 0xFF, 8 * (size_t)n, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(ppg_block_find_kernel, dim3(n, sub), dim3(64), 0, s, comp, nwords, lo, hi, cand, n);
     return hipGetLastError();
 }
 

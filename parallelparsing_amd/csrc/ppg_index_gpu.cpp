@@ -50,7 +50,7 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs);
 hipError_t ppg_launch_block_find(hipStream_t s, const uint32_t *comp, uint64_t nwords, const uint64_t *lo,
-                                 const uint64_t *hi, uint64_t *cand, int n);
+                                 const uint64_t *hi, uint64_t *cand, int n, int sub);
 hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
                              const uint8_t *ref, uint32_t *diff, int n);
 hipError_t ppg_launch_at_stats(hipStream_t s, const uint8_t *out, const PpgSpan *spans, PpgAtStats *st, int n);
@@ -332,7 +332,7 @@ static int build_index_gpu(ppg_ctx *ctx, const uint8_t *dcomp, int64_t len, cons
         if (!lo.empty()) {
             HIPCHK(hipMemcpyAsync(dlo.p, lo.data(), 8 * lo.size(), hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(dhi.p, hi.data(), 8 * lo.size(), hipMemcpyHostToDevice, s));
-            HIPCHK(ppg_launch_block_find(s, B.comp, B.nwords, dlo.p, dhi.p, dc.p, (int)lo.size()));
+            HIPCHK(ppg_launch_block_find(s, B.comp, B.nwords, dlo.p, dhi.p, dc.p, (int)lo.size(), 1));
             HIPCHK(hipMemcpyAsync(cand.data(), dc.p, 8 * lo.size(), hipMemcpyDeviceToHost, s));
         }
         HIPCHK(hipStreamSynchronize(s));

@@ -355,10 +355,10 @@ __device__ __forceinline__ void flush_census(const uint8_t *ring, uint8_t *out, 
 // an aligned dword from a uniform base + 32-bit lane offset (global_load saddr form; never merged
 // with an LDS byte load into a flat load).  ob: out + (out_off & ~3), oa: out_off & 3.
 // IX (CreateIndex pass 1): the job's output is a 64 KiB ring, position p at ob[p & 0xFFFF].
-template <bool IX = false>
+template <bool IX = false, uint32_t IXM = IX_RING_MASK>
 __device__ __forceinline__ uint32_t far_byte(const uint8_t *ob, uint32_t oa, const uint8_t *dict, int32_t p) {
-    if constexpr (IX) {   // 16-bit symbols: the job's ring, or the history index itself
-        if (p >= 0) return ((const uint16_t *)ob)[(uint32_t)p & IX_RING_MASK];
+    if constexpr (IX) {   // 16-bit symbols: the job's ring (IXM; ~0: its whole output), or the history index itself
+        if (p >= 0) return ((const uint16_t *)ob)[(uint32_t)p & IXM];
         return 32768u + (uint32_t)p;
     } else {
         // the two loads differ in width so the compiler cannot fold them into one per-lane base select
@@ -392,7 +392,7 @@ __device__ __forceinline__ uint32_t far_load_u8(const uint8_t *base, uint32_t of
 }
 
 // One LZ77 copy of n bytes from dist back, at chunk position pos (all 64 lanes, uniform args).
-template <int RB, bool IX, typename RingT>
+template <int RB, bool IX, typename RingT, uint32_t IXM = IX_RING_MASK>
 __device__ __forceinline__ void copy_match(RingT *ring, const uint8_t *ob, uint32_t oa, const uint8_t *dict,
                                            uint32_t rb0, uint32_t pos, uint32_t dist, uint32_t n, int lane) {
     constexpr uint32_t RM = (1u << RB) - 1;
@@ -423,7 +423,7 @@ __device__ __forceinline__ void copy_match(RingT *ring, const uint8_t *ob, uint3
                 const int32_t rel = (int32_t)pos - (int32_t)back;
                 uint32_t v;
                 if (back + n <= REACH) v = ring[(dst0 - back) & RM];
-                else v = far_byte<IX>(ob, oa, dict, rel);
+                else v = far_byte<IX, IXM>(ob, oa, dict, rel);
                 ring[(dst0 + j) & RM] = (RingT)v;
             }
         }
@@ -534,7 +534,11 @@ __device__ __forceinline__ uint32_t latch_limit(uint32_t x, uint32_t lim) {
 // profiles/r03_ab_latch_sj.txt).
 // amdgpu_waves_per_eu(8, 8): the VGPRs held to 64 (r04: the round loop's carry state took the
 // compiler to 65, 7 waves per SIMD)
-template <int RB, int LBT, bool IX, bool CEN>
+// IXF (CreateIndex-style pass 1 with IX = true): each job's symbolic output is kept whole at
+// out + 2 * out_off (J.out_len = its capacity in positions; past it the job fails) instead of a
+// 64 Ki-position ring -- the lone-chunk Decompress materialises its pieces from it
+// (ppg_materialize_kernel) instead of decoding them a second time
+template <int RB, int LBT, bool IX, bool CEN, bool IXF = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void ppg_inflate_kernel(const uint32_t *__restrict__ comp, uint64_t nwords,
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
@@ -547,6 +551,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     constexpr uint32_t UNIT = RB >= 13 ? 4096u : RING / 2;
     static_assert(RB >= 10 && RB <= 15, "ring of 1..32 KiB");
     using RingT = typename std::conditional<IX, uint16_t, uint8_t>::type;   // IX: 16-bit symbols
+    constexpr uint32_t IXM = IXF ? 0xFFFFFFFFu : IX_RING_MASK;             // IX output: ring or whole
+    static_assert(!IXF || IX, "IXF is a pass-1 (IX) form");
     // static LDS: every address is a link-time constant the compiler folds into the instructions'
     // offsets (a dynamic extern array cost one v_add of its base per ring access, r03)
     __shared__ InflateLds<RB, LBT, RingT> S;
@@ -556,6 +562,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     const PpgInflateJob J = jobs[k];
     const uint64_t out_off = J.out_off;
     const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // < 2^31: ppg_index_validate
+    // IX: past this many positions the job is a runaway (a false start); IXF: its output's capacity
+    const uint32_t ixcap = IXF ? (uint32_t)J.out_len : 0xF0000000u;
     const uint32_t rb0 = (uint32_t)out_off;         // ring slot of chunk position p: (rb0 + p) & RM
     const uint8_t *dict = dicts + J.dict_off;       // chunk position p < 0 is dict[32768 + p]
     // chunk position p >= 0 is ob[oa + p] (IX: 16-bit symbol ((uint16_t *)ob)[p & IX_RING_MASK])
@@ -627,7 +635,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if (b) ix_last = p0 + 64u - (uint32_t)__clzll(b);
             }
 #endif
-            const uint64_t g = out_off + (lo & IX_RING_MASK);
+            const uint64_t g = out_off + (lo & IXM);
             flush_range_sym<RB>(S.ring, (uint16_t *)out, g, g + (hi - lo), lane);
         } else {
             if constexpr (census) {
@@ -925,7 +933,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                     const int32_t p = (int32_t)pos + jj;
                     const bool fo = far && p >= 0;
                     if constexpr (IX) {
-                        const uint32_t q = 2u * ((uint32_t)p & IX_RING_MASK);
+                        const uint32_t q = 2u * ((uint32_t)p & IXM);
                         const uint32_t w = far_load(ob, fo ? (q & ~3u) : 0u);
                         val = fo ? __builtin_amdgcn_ubfe(w, q << 3, 16u) : val;
                     } else {
@@ -980,7 +988,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             bp += R.adv;
             asm volatile("s_setprio 0");
             if constexpr (IX) {   // past the member, or runaway output (a false start)
-                if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; return 128u; }
+                if (bp > bit_limit || pos > ixcap) { status = ST_DATA_ERROR; return 128u; }
             }
 #ifdef PPG_STAMPS
             sa_tail += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)bp - st_w0;
@@ -1011,7 +1019,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             auto finish = [&]() {
                 uint32_t val = p_val;
                 if constexpr (IX) {   // CreateIndex pass 1: the 16-bit symbol in the loaded dword
-                    const uint32_t q = 2u * ((p_pos + (uint32_t)p_jj) & IX_RING_MASK);
+                    const uint32_t q = 2u * ((p_pos + (uint32_t)p_jj) & IXM);
                     uint32_t fv = __builtin_amdgcn_ubfe(p_b, q << 3, 16u);
                     if constexpr (EARLY) {   // before the piece: the history symbol itself
                         const int32_t p = (int32_t)p_pos + p_jj;
@@ -1107,7 +1115,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 // pos >= 32768: every far source is the flushed output; a compiler-tracked load (its
                 // s_waitcnt lands at the first use, in finish)
                 if constexpr (IX) {   // the job's 64 Ki-symbol ring, as the dword holding the symbol
-                    const uint32_t q = 2u * ((pos + (uint32_t)jj) & IX_RING_MASK);
+                    const uint32_t q = 2u * ((pos + (uint32_t)jj) & IXM);
                     const bool ld = EARLY ? far && (int32_t)pos + jj >= 0 : far;
                     p_b = *(const uint32_t *)(ob + (uint64_t)(ld ? (q & ~3u) : 0u));
                 } else if constexpr (EARLY) {
@@ -1127,7 +1135,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 asm volatile("s_setprio 0");
                 lim_r = latch_limit(R.xr, limh);
                 if constexpr (IX) {   // past the member, or runaway output (a false start)
-                    if (bp > bit_limit || pos > 0xF0000000u) { status = ST_DATA_ERROR; lim_r = 0; }
+                    if (bp > bit_limit || pos > ixcap) { status = ST_DATA_ERROR; lim_r = 0; }
                 }
 #ifdef PPG_STAMPS
                 hs_emit += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(p_b + lim_r) - h4;
@@ -1206,7 +1214,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
                 const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
                 const uint32_t n = min(ml, len - pos);
-                copy_match<RB, IX, RingT>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
+                copy_match<RB, IX, RingT, IXM>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
             }
             bp = rd_pos(r);
@@ -1380,3 +1388,83 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
 #ifdef PPG_STAMPS
 static void ppg_stamp_dump(hipStream_t s) { PpgStampPrinter::dump(s); }
 #endif
+
+// the lone-chunk Decompress's pass 1 (ppg_chunk.cpp): symbolic output kept whole per job (IXF)
+hipError_t ppg_launch_inflate_ixf(hipStream_t s, const uint32_t *comp, uint64_t nwords, const PpgInflateJob *jobs,
+                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
+                                  int njobs) {
+    if (njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false, true>), dim3(njobs), dim3(64), 0, s, comp, nwords, jobs,
+                       dicts, out, res, njobs, blk, nullptr);
+    return hipGetLastError();
+}
+
+// A piece whose pass-1 symbols and exact starting history are known is written out without a second
+// decode: symbol 0x8000 | b is the byte b, symbol i < 32768 is byte i of the history.  The bytes go
+// through the inflate kernel's own flush path -- a 1 KiB LDS ring by global output address, flushed
+// in aligned 512-B units with the fused newline census (flush_census) -- so the piece's result and
+// census region are exactly what decoding it (ppg_inflate_kernel, CEN) would have produced.
+// mi[k].prev: the census's "previous byte" (a chunk's first piece: the job's own, from the Point's
+// offset), or > 255: the history's last byte.
+template <int RB>
+__global__ __launch_bounds__(64) void ppg_materialize_kernel(const uint16_t *__restrict__ sym,
+                                                             const uint8_t *__restrict__ wins,
+                                                             const PpgMatInfo *__restrict__ mi,
+                                                             const PpgInflateJob *__restrict__ jobs,
+                                                             uint8_t *__restrict__ out, PpgInflateResult *__restrict__ res,
+                                                             int njobs, uint32_t *__restrict__ nls) {
+    constexpr uint32_t RING = 1u << RB, RM = RING - 1, UNIT = RING / 2;
+    __shared__ __attribute__((aligned(16))) uint8_t W[32768];
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
+    __shared__ uint32_t cen[8];
+    const int k = blockIdx.x, lane = threadIdx.x;
+    if (k >= njobs) return;
+    const PpgInflateJob J = jobs[k];
+    const PpgMatInfo M = mi[k];
+    for (uint32_t i = 16u * (uint32_t)lane; i < 32768u; i += 1024u)
+        *(uint4 *)&W[i] = *(const uint4 *)(wins + M.win_off + i);
+    __syncthreads();
+    if (lane == 0) {
+        const uint64_t d = (uint64_t)(uintptr_t)(nls + J.nl_off);
+        cen[0] = 0;
+        cen[1] = (M.prev > 255u ? W[32767] : M.prev) == '\n';
+        cen[2] = 0;
+        cen[3] = J.nl_cap;
+        cen[4] = J.raw_shift;
+        cen[5] = (uint32_t)d;
+        cen[6] = (uint32_t)(d >> 32);
+    }
+    __syncthreads();
+    const uint32_t len = (uint32_t)J.out_len;
+    const uint64_t out_off = J.out_off;
+    const uint16_t *sy = sym + M.sym_off;
+    for (uint32_t p0 = 0; p0 < len;) {
+        const uint32_t p1 = min(len, p0 + (UNIT - (uint32_t)((out_off + p0) & (UNIT - 1))));
+        for (uint32_t p = p0 + (uint32_t)lane; p < p1; p += 64) {
+            const uint32_t v = sy[p];
+            ring[(uint32_t)(out_off + p) & RM] = (uint8_t)((v & 0x8000u) ? v : W[v & 32767u]);
+        }
+        __syncthreads();
+        flush_census<RB>(ring, out, out_off, p0, p1, lane, cen);
+        __syncthreads();
+        p0 = p1;
+    }
+    if (lane == 0) {
+        res[k].produced = len;
+        res[k].end_bit = M.end_bit;
+        res[k].status = 0;
+        res[k].flags = 0;
+        res[k].nblocks = M.nblocks;
+        res[k].last = M.last;
+        res[k].newlines = cen[0];
+        res[k].pflags = cen[2];
+    }
+}
+
+hipError_t ppg_launch_materialize(hipStream_t s, const uint16_t *sym, const uint8_t *wins, const PpgMatInfo *mi,
+                                  const PpgInflateJob *jobs, uint8_t *out, PpgInflateResult *res, int njobs,
+                                  uint32_t *nls) {
+    if (njobs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_materialize_kernel<10>, dim3(njobs), dim3(64), 0, s, sym, wins, mi, jobs, out, res, njobs, nls);
+    return hipGetLastError();
+}

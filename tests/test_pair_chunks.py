@@ -117,7 +117,7 @@ def test_pair_chunks_one_rank(pair_files, device, K, cap, window):
     ix = [pp.Core.BuildDeflateIndex(g, c) for g, c in zip(gz, chunks)]
     sh = [shard_of(g, i, device, cap) for g, i in zip(gz, ix)]
     if cap:
-        assert sh[0].batches > 4 and sh[1].batches > 4
+        assert sh[0].batches >= 3 and sh[1].batches >= 3
     pr = paired.Pairs()
     res = pr.check(sh[0], sh[1])
     assert res["pairs"] == nrec and res["mismatches"] == 0 and res["duplicates"][0] == recs[0][1]

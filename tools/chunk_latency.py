@@ -17,7 +17,7 @@ import parallelparsing_amd as pp   # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--records", type=int, default=400_000)
+    ap.add_argument("--records", type=int, default=2_600_000)
     ap.add_argument("--chunk", type=int, default=10_000)
     ap.add_argument("--threads", default="1,8,64")
     args = ap.parse_args()

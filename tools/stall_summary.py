@@ -37,7 +37,7 @@ def main(tag):
     c = passes()
     wc = c["SQ_WAVE_CYCLES"]
     out = {
-        "kernel": "ppg_inflate_kernel<10, 8, false, true>",
+        "kernel": "ppg_inflate_kernel<10, 8, false, true, false>",
         "workload": "bench.py --repeats 40 --steps 1 (40 x 4.04 GB text, chunk = 10,000), one launch",
         "command": "tools/pmc_stalls.sh: one rocprofv3 --pmc pass per counter group (A-E)",
         "counters": c,
