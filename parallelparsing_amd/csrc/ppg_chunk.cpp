@@ -35,9 +35,9 @@ hipError_t ppg_launch_inflate_ixf(hipStream_t s, const uint32_t *comp, uint64_t 
                                   int njobs);
 hipError_t ppg_launch_gather(hipStream_t s, const uint8_t *out, const uint8_t *dicts, const PpgGather *g, uint8_t *dst,
                              const uint8_t *ref, uint32_t *diff, int n);
-hipError_t ppg_launch_resolve(hipStream_t s, const uint8_t *ta, const uint8_t *tb, const uint32_t *slots, int np,
-                              uint8_t *W, uint16_t *M);
-int ppg_resolve_groups(int np);
+hipError_t ppg_launch_resolve_chains(hipStream_t s, const uint8_t *ta, const uint32_t *slots, const uint4 *chains,
+                                     int nchains, const uint8_t *windows, uint8_t *W);
+hipError_t ppg_launch_pick_windows(hipStream_t s, const uint8_t *src, const uint32_t *idx, int n, uint8_t *dst);
 
 namespace {
 
@@ -72,6 +72,11 @@ struct ChunkReq {
     int64_t got = 0;
     const uint32_t *src_recs = nullptr;
     int64_t nrec = 0;
+    // an async request's results already copied into out/recs by the launcher (fin_*: what wait() returns)
+    bool copied = false;
+    int fin_rc = PPG_OK;
+    int64_t fin_len = 0;
+    bool fin_nrec = false;
 };
 
 // grow a buffer to `need` elements, by at least half again its size (no reallocation per call)
@@ -79,6 +84,63 @@ template <class B>
 hipError_t grow_buf(B &b, size_t need) {
     if (b.p && b.n >= need) return hipSuccess;
     return b.alloc(std::max(need, b.n + b.n / 2));
+}
+
+// memcpy of many (dst, src, len) spans: on the calling thread when small, else spread over up to
+// 8 threads in 1 MiB pieces -- a launch gathers up to 1,024 slices into the pinned staging buffer and
+// the async path copies up to a GiB of results into fresh caller pages (page faults included), which
+// one thread does at a few GB/s
+struct Span {
+    uint8_t *dst;
+    const uint8_t *src;
+    size_t len;
+};
+
+void parallel_copy(const std::vector<Span> &v) {
+    constexpr size_t kPiece = 1 << 20;
+    size_t tot = 0;
+    for (const Span &x : v) tot += x.len;
+    if (tot < 8 * kPiece) {
+        for (const Span &x : v)
+            if (x.len) memcpy(x.dst, x.src, x.len);
+        return;
+    }
+    std::vector<Span> pieces;
+    for (const Span &x : v)
+        for (size_t o = 0; o < x.len; o += kPiece) pieces.push_back(Span{x.dst + o, x.src + o, std::min(kPiece, x.len - o)});
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t i; (i = next.fetch_add(1)) < pieces.size();) memcpy(pieces[i].dst, pieces[i].src, pieces[i].len);
+    };
+    std::vector<std::thread> th;
+    const size_t nt = std::min<size_t>(8, tot / (4 * kPiece));
+    try {
+        for (size_t t = 1; t < nt; t++) th.emplace_back(work);
+    } catch (...) {   // no threads: the calling thread copies everything
+    }
+    work();
+    for (auto &t : th) t.join();
+}
+
+// What a decoded request hands its caller: the status (PPG_BUF_ERROR when a buffer is too small),
+// the byte count, whether the record count is reported, and the copies out of the slot's results.
+int result_spans(const ChunkReq &req, uint8_t *out, int64_t out_cap, uint32_t *recs, int64_t rec_cap, int64_t &len,
+                 bool &with_nrec, std::vector<Span> &cp) {
+    len = req.got;
+    with_nrec = false;
+    if (out) {
+        if (req.got > out_cap) {
+            len = 0;
+            return PPG_BUF_ERROR;
+        }
+        if (req.got) cp.push_back(Span{out, req.src, (size_t)req.got});
+    }
+    with_nrec = true;
+    if (recs) {
+        if (req.nrec > rec_cap) return PPG_BUF_ERROR;
+        if (req.nrec) cp.push_back(Span{(uint8_t *)recs, (const uint8_t *)req.src_recs, 16 * (size_t)req.nrec});
+    }
+    return PPG_OK;
 }
 
 // waves per candidate range of the block search: enough for ~4,096 waves in all (a lone chunk's 16
@@ -97,8 +159,9 @@ struct FindScratch {
     DevBuf<PpgBlockEnd> blk;
     DevBuf<uint8_t> ring, ta, ident, W;
     DevBuf<PpgGather> gat;
-    DevBuf<uint32_t> slots;
-    DevBuf<uint16_t> maps;
+    DevBuf<uint32_t> slots, pick;
+    DevBuf<uint4> chains;
+    DevBuf<uint8_t> packed;
 };
 
 struct ChunkSlot {
@@ -223,10 +286,11 @@ struct FindChunk {
     uint64_t bit_end;                   // to's block start (8 to.Input - to.Bits), or bit1 for the last chunk
     int64_t out0;                       // the chunk's first output byte (launch coordinates)
     int64_t len;                        // the chunk's output bytes
-    const uint8_t *window;              // the Point's 32 KiB
+    uint32_t win;                       // the Point's 32 KiB: window `win` of the shard's device dicts
 };
 
-int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const std::vector<FindChunk> &ch,
+int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t *dwin,
+                     const std::vector<FindChunk> &ch,
                      std::vector<int64_t> &sbit, std::vector<int64_t> &sout, ByteVec &swin, int64_t &nsplit,
                      PhaseClock &clk) {
     hipStream_t s = sl.s;
@@ -340,46 +404,45 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
             if (q + 1 >= pfirst[c + 1] || pc[q + 1].start != E) break;   // the next candidate was false
         }
     }
-    // histories at the verified block ends: W[0] = the Point's window, W[j+1] = T_j(W[j])
-    size_t wmax = 0, cmax = 0;
-    for (size_t c = 0; c < ch.size(); c++) {
-        wmax = std::max(wmax, chain[c].size() + 1);
-        cmax = std::max(cmax, chain[c].size());
-    }
-    if (!cmax) return PPG_OK;
+    // histories at the verified block ends, every chain in one launch: W[0] = the Point's window,
+    // W[j+1] = T_j(W[j]); the kept ones packed on the device and copied back at once
+    size_t wmax = 0;
+    for (size_t c = 0; c < ch.size(); c++) wmax = std::max(wmax, chain[c].size() + 1);
+    if (wmax < 2) return PPG_OK;
     HIPCHK(grow_buf(F.W, ch.size() * wmax * kWin));
     HIPCHK(grow_buf(F.slots, ch.size() * wmax));
-    HIPCHK(grow_buf(F.maps, (size_t)ppg_resolve_groups((int)cmax) * kWin));
     std::vector<uint32_t> sl_all(ch.size() * wmax, 0);
-    for (size_t c = 0; c < ch.size(); c++)
-        std::copy(chain[c].begin(), chain[c].end(), sl_all.begin() + (ptrdiff_t)(c * wmax));
-    HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * sl_all.size(), hipMemcpyHostToDevice, s));
+    std::vector<uint4> cs;
     for (size_t c = 0; c < ch.size(); c++) {
         if (chain[c].empty()) continue;
-        uint8_t *W = F.W.p + c * wmax * kWin;
-        HIPCHK(hipMemcpyAsync(W, ch[c].window, kWin, hipMemcpyHostToDevice, s));
-        HIPCHK(ppg_launch_resolve(s, F.ta.p, nullptr, F.slots.p + c * wmax, (int)chain[c].size(), W, F.maps.p));
+        std::copy(chain[c].begin(), chain[c].end(), sl_all.begin() + (ptrdiff_t)(c * wmax));
+        cs.push_back(uint4{(uint32_t)(c * wmax), (uint32_t)chain[c].size() + 1, ch[c].win, 0});
     }
+    HIPCHK(grow_buf(F.chains, cs.size()));
+    HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * sl_all.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(F.chains.p, cs.data(), sizeof(uint4) * cs.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_resolve_chains(s, F.ta.p, F.slots.p, F.chains.p, (int)cs.size(), dwin, F.W.p));
     const size_t base = sbit.size();
-    size_t nnew = 0;
-    for (size_t c = 0; c < ch.size(); c++)
-        for (const End &e : ends[c]) nnew += e.keep;
-    swin.resize((base + nnew) * kWin);
-    size_t t = base;
+    std::vector<uint32_t> pick;
     for (size_t c = 0; c < ch.size(); c++) {
         bool any = false;
         for (size_t j = 0; j < ends[c].size(); j++) {
             const End &e = ends[c][j];
             if (!e.keep) continue;
-            // W[j + 1]: the history at the end of chain piece j (an empty block adds none)
-            HIPCHK(hipMemcpyAsync(swin.data() + t * kWin, F.W.p + (c * wmax + j + 1) * kWin, kWin,
-                                  hipMemcpyDeviceToHost, s));
+            pick.push_back((uint32_t)(c * wmax + j + 1));   // W[j + 1]: the history at the end of chain piece j
             sbit.push_back((int64_t)e.bit);
             sout.push_back(ch[c].out0 + (int64_t)e.out);
-            t++;
             any = true;
         }
         nsplit += any;
+    }
+    swin.resize((base + pick.size()) * kWin);
+    if (!pick.empty()) {
+        HIPCHK(grow_buf(F.pick, pick.size()));
+        HIPCHK(grow_buf(F.packed, pick.size() * kWin));
+        HIPCHK(hipMemcpyAsync(F.pick.p, pick.data(), 4 * pick.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(ppg_launch_pick_windows(s, F.W.p, F.pick.p, (int)pick.size(), F.packed.p));
+        HIPCHK(hipMemcpyAsync(swin.data() + base * kWin, F.packed.p, pick.size() * kWin, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     clk.mark("f.resolve");
@@ -404,7 +467,7 @@ struct MatPiece {
     uint64_t sym_off, cap;      // symbols
 };
 
-int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const std::vector<FindChunk> &ch,
+int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t *dwin, const std::vector<FindChunk> &ch,
              std::vector<uint8_t> &covered, std::vector<std::vector<PpgMatInfo>> &pmi,
              std::vector<std::vector<int64_t>> &pbit, std::vector<std::vector<int64_t>> &pout, PhaseClock &clk) {
     hipStream_t s = sl.s;
@@ -533,24 +596,19 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const std::ve
     HIPCHK(grow_buf(F.gat, 2 * np));
     HIPCHK(hipMemcpyAsync(F.gat.p, g.data(), sizeof(PpgGather) * 2 * np, hipMemcpyHostToDevice, s));
     HIPCHK(ppg_launch_gather(s, (const uint8_t *)F.sym.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * np)));
-    size_t cmax = 0;
-    for (size_t c = 0; c < ch.size(); c++)
-        if (covered[c]) cmax = std::max(cmax, pfirst[c + 1] - pfirst[c]);
     HIPCHK(grow_buf(F.W, nw * kWin));
     HIPCHK(grow_buf(F.slots, nw));
-    HIPCHK(grow_buf(F.maps, (size_t)ppg_resolve_groups((int)cmax) * kWin));
     std::vector<uint32_t> sl_all(nw, 0);
-    for (size_t c = 0; c < ch.size(); c++)
-        if (covered[c])
-            for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) sl_all[wbase[c] + (q - pfirst[c])] = (uint32_t)q;
-    HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * nw, hipMemcpyHostToDevice, s));
+    std::vector<uint4> cs;
     for (size_t c = 0; c < ch.size(); c++) {
         if (!covered[c]) continue;
-        uint8_t *W = F.W.p + wbase[c] * kWin;
-        HIPCHK(hipMemcpyAsync(W, ch[c].window, kWin, hipMemcpyHostToDevice, s));
-        const size_t m = pfirst[c + 1] - pfirst[c];
-        if (m > 1) HIPCHK(ppg_launch_resolve(s, F.ta.p, nullptr, F.slots.p + wbase[c], (int)(m - 1), W, F.maps.p));
+        for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) sl_all[wbase[c] + (q - pfirst[c])] = (uint32_t)q;
+        cs.push_back(uint4{(uint32_t)wbase[c], (uint32_t)(pfirst[c + 1] - pfirst[c]), ch[c].win, 0});
     }
+    HIPCHK(grow_buf(F.chains, cs.size()));
+    HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * nw, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(F.chains.p, cs.data(), sizeof(uint4) * cs.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_resolve_chains(s, F.ta.p, F.slots.p, F.chains.p, (int)cs.size(), dwin, F.W.p));
     // the pieces' materialise info, side points at every later piece's start (launch coordinates)
     for (size_t c = 0; c < ch.size(); c++) {
         if (!covered[c]) continue;
@@ -645,8 +703,15 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     }
     HIPCHK(grow_buf(sl.in, comp_len + 256));
     HIPCHK(grow_buf(sl.comp, comp_len + 256));
-    memset(sl.in.p, 0, comp_len + 256);
-    for (size_t i = 0; i < go.size(); i++) memcpy(sl.in.p + at[i], go[i]->slice, (size_t)go[i]->slice_len);
+    {   // the slices, the alignment gaps and the 256-B tail zeroed (the kernels read whole words past a slice)
+        std::vector<Span> cp;
+        for (size_t i = 0; i < go.size(); i++) {
+            const size_t end = (size_t)at[i] + (size_t)go[i]->slice_len;
+            memset(sl.in.p + end, 0, (i + 1 < go.size() ? (size_t)at[i + 1] : comp_len + 256) - end);
+            cp.push_back(Span{sl.in.p + at[i], go[i]->slice, (size_t)go[i]->slice_len});
+        }
+        parallel_copy(cp);
+    }
     HIPCHK(hipMemcpyAsync(sl.comp.p, sl.in.p, comp_len + 256, hipMemcpyHostToDevice, sl.s));
     ppg_shard *sh = sl.sh;
     pc.mark("h2d", sl.s);
@@ -660,12 +725,12 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
         for (size_t i = 0; i < go.size(); i++) {
             const PpgInflateJob &J = sh->h_jobs[i];
             find.push_back(FindChunk{J.bit_start, J.bit_limit, J.expect_end != ~0ull ? J.expect_end : J.bit_limit,
-                                     sh->h_pout[i], (int64_t)J.out_len, go[i]->ix->win((size_t)go[i]->k)});
+                                     sh->h_pout[i], (int64_t)J.out_len, (uint32_t)i});
         }
         std::vector<uint8_t> covered;
         std::vector<std::vector<PpgMatInfo>> pmi;
         std::vector<std::vector<int64_t>> pbit, pout;
-        rc = find_mat(sl, (const uint32_t *)sl.comp.p, sh->nwords, find, covered, pmi, pbit, pout, pc);
+        rc = find_mat(sl, (const uint32_t *)sl.comp.p, sh->nwords, sh->dicts.p, find, covered, pmi, pbit, pout, pc);
         if (rc != PPG_OK) return rc;
         std::vector<int64_t> sbit, sout;
         size_t ncov = 0;
@@ -734,12 +799,12 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
                 // sorted by output with the others: flush the found ones in launch order
                 const PpgInflateJob &J = sh->h_jobs[i];
                 find.push_back(FindChunk{J.bit_start, J.bit_limit, J.expect_end != ~0ull ? J.expect_end : J.bit_limit,
-                                         sh->h_pout[i], (int64_t)J.out_len, go[i]->ix->win((size_t)go[i]->k)});
+                                         sh->h_pout[i], (int64_t)J.out_len, (uint32_t)i});
             }
             if (!find.empty() && (i + 1 == go.size() || !go[i + 1]->ix->side_out.empty())) {
                 const size_t before = sbit.size();
                 int64_t nsplit = 0;
-                rc = find_side_points(sl, (const uint32_t *)sl.comp.p, sh->nwords, find, sbit, sout, swin, nsplit, pc);
+                rc = find_side_points(sl, (const uint32_t *)sl.comp.p, sh->nwords, sh->dicts.p, find, sbit, sout, swin, nsplit, pc);
                 if (rc != PPG_OK) return rc;
                 svc.found_chunks += nsplit;
                 svc.found_points += (int64_t)(sbit.size() - before);
@@ -821,6 +886,14 @@ void lead(ppg_ctx *ctx, ChunkService &svc, std::unique_lock<std::mutex> &lk, int
     int rc;
     try {
         rc = run_launch(ctx, svc, sl, batch);
+        if (rc == PPG_OK) {   // async requests: copied out here, all at once, so wait() only hands back
+            std::vector<Span> cp;
+            for (ChunkReq *r : batch)
+                if (r->async && r->rc == PPG_OK)
+                    r->fin_rc = result_spans(*r, r->out, r->out_cap, r->recs, r->rec_cap, r->fin_len, r->fin_nrec, cp);
+            parallel_copy(cp);
+            for (ChunkReq *r : batch) r->copied = r->async && r->rc == PPG_OK;
+        }
     } catch (const std::bad_alloc &) {   // host vectors: never out through the C ABI, never a stuck slot
         rc = PPG_MEM_ERROR;
     } catch (...) {
@@ -829,7 +902,8 @@ void lead(ppg_ctx *ctx, ChunkService &svc, std::unique_lock<std::mutex> &lk, int
     lk.lock();
     for (ChunkReq *r : batch) {
         if (rc != PPG_OK) r->rc = rc;
-        if (r->rc == PPG_OK) {
+        if (rc != PPG_OK) r->copied = false;
+        if (r->rc == PPG_OK && !r->copied) {
             r->slot = i;
             sl.readers++;
         }
@@ -843,25 +917,24 @@ void lead(ppg_ctx *ctx, ChunkService &svc, std::unique_lock<std::mutex> &lk, int
 // copy a done request's results out of its slot (callers copy in parallel), release the slot
 int finish(ChunkService &svc, ChunkReq &req, uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs,
            int64_t rec_cap, int64_t *nrec) {
+    if (req.copied) {   // an async request the launcher already copied out
+        if (produced) *produced = req.fin_len;
+        if (nrec && req.fin_nrec) *nrec = req.nrec;
+        return req.fin_rc;
+    }
     int rc = req.rc;
     if (rc == PPG_OK) {
-        int64_t len = req.got;
-        if (out) {
-            if (req.got > out_cap) {
-                rc = PPG_BUF_ERROR;
-                len = 0;
-            } else if (req.got) {
-                memcpy(out, req.src, (size_t)req.got);
-            }
+        int64_t len = 0;
+        bool with_nrec = false;
+        std::vector<Span> cp;
+        try {
+            rc = result_spans(req, out, out_cap, recs, rec_cap, len, with_nrec, cp);
+            parallel_copy(cp);
+        } catch (...) {
+            rc = PPG_MEM_ERROR;
         }
         if (produced) *produced = len;
-        if (rc == PPG_OK) {
-            if (nrec) *nrec = req.nrec;
-            if (recs) {
-                if (req.nrec > rec_cap) rc = PPG_BUF_ERROR;
-                else if (req.nrec) memcpy(recs, req.src_recs, 16 * (size_t)req.nrec);
-            }
-        }
+        if (nrec && with_nrec) *nrec = req.nrec;
         std::lock_guard<std::mutex> lk(svc.mu);
         if (--svc.slot[req.slot].readers == 0) svc.cv.notify_all();
     }

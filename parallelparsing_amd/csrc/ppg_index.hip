@@ -404,6 +404,63 @@ __global__ __launch_bounds__(1024) void ppg_resolve_fill_kernel(const uint8_t *_
     }
 }
 
+// Many short chains at once (the per-chunk Decompress path, ppg_chunk.cpp find_mat: one chain per
+// chunk of ~16 pieces, up to 256 chunks a launch): one workgroup per chain, its steps serial with the
+// current history in LDS -- composing maps only pays for one long chain.  chains[c] = {wb, m, src}:
+//   W[wb] = windows[src],  W[wb + j + 1] = T_{slots[wb + j]}(W[wb + j]),  j < m - 1.
+__global__ __launch_bounds__(1024) void ppg_resolve_chains_kernel(const uint8_t *__restrict__ ta,
+                                                                  const uint32_t *__restrict__ slots,
+                                                                  const uint4 *__restrict__ chains,
+                                                                  const uint8_t *__restrict__ windows, uint8_t *W) {
+    __shared__ uint32_t h[2][8192];
+    const uint4 c = chains[blockIdx.x];
+    const uint32_t *src = (const uint32_t *)(windows + (uint64_t)c.z * 32768);
+    uint32_t *w0 = (uint32_t *)(W + (uint64_t)c.x * 32768);
+    for (uint32_t t = threadIdx.x; t < 8192; t += 1024) {
+        const uint32_t v = src[t];
+        h[0][t] = v;
+        w0[t] = v;
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j + 1 < c.y; j++) {
+        const uint8_t *cur = (const uint8_t *)h[j & 1];
+        uint32_t *nx = h[(j + 1) & 1];
+        uint32_t *d = (uint32_t *)(W + (uint64_t)(c.x + j + 1) * 32768);
+        const uint32_t slot = slots[c.x + j];
+#pragma unroll 2
+        for (uint32_t t = threadIdx.x; t < 8192; t += 1024) {
+            uint32_t e[4], v = 0;
+            tail4(ta, nullptr, slot, t, e);
+#pragma unroll
+            for (int q = 0; q < 4; q++) v |= (e[q] & 0x8000u ? e[q] & 255u : (uint32_t)cur[e[q]]) << (8 * q);
+            nx[t] = v;
+            d[t] = v;
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t ppg_launch_resolve_chains(hipStream_t s, const uint8_t *ta, const uint32_t *slots, const uint4 *chains,
+                                     int nchains, const uint8_t *windows, uint8_t *W) {
+    if (nchains <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_resolve_chains_kernel, dim3(nchains), dim3(1024), 0, s, ta, slots, chains, windows, W);
+    return hipGetLastError();
+}
+
+// dst window i = src window idx[i] (32 KiB each): the kept histories of many chains, packed for one copy
+__global__ __launch_bounds__(256) void ppg_pick_windows_kernel(const uint8_t *__restrict__ src,
+                                                               const uint32_t *__restrict__ idx, uint8_t *dst) {
+    const uint4 *s = (const uint4 *)(src + (uint64_t)idx[blockIdx.x] * 32768);
+    uint4 *d = (uint4 *)(dst + (uint64_t)blockIdx.x * 32768);
+    for (uint32_t t = threadIdx.x; t < 2048; t += 256) d[t] = s[t];
+}
+
+hipError_t ppg_launch_pick_windows(hipStream_t s, const uint8_t *src, const uint32_t *idx, int n, uint8_t *dst) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ppg_pick_windows_kernel, dim3(n), dim3(256), 0, s, src, idx, dst);
+    return hipGetLastError();
+}
+
 // W[1..np] from W[0] (zeroed by the caller); M: scratch of ppg_resolve_groups(np) x 32768 u16
 int ppg_resolve_groups(int np) {
     int g = 1;

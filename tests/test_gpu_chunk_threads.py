@@ -222,6 +222,8 @@ def test_async_submit_vs_oracle(file200k):
     before = dev.decompress_chunk_stats()
     futs = [(k, pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, k), ix, k, device=dev)) for k in list(range(n)) * 2]
     bad = pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, 3)[:-1], ix, 3, device=dev)   # short slice
+    # too small a buffer: the launcher copies async results out itself (r05) -- BUF_ERROR, alone
+    small = pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, 5), ix, 5, buf=np.zeros(10, np.uint8), device=dev)
     for k, f in futs:
         got, buf, rec = f.result()
         assert sha(buf[:got]) == exp[k][0], k
@@ -229,9 +231,12 @@ def test_async_submit_vs_oracle(file200k):
     with pytest.raises(pp.PpgError) as e:
         bad.result()
     assert e.value.code == _lib.PPG_ARG_ERROR
+    with pytest.raises(pp.PpgError) as e:
+        small.result()
+    assert e.value.code == _lib.PPG_BUF_ERROR
     st = dev.decompress_chunk_stats()
     calls, launches = st["calls"] - before["calls"], st["launches"] - before["launches"]
-    assert calls == 2 * n + 1 and launches <= 8, (calls, launches, st)
+    assert calls == 2 * n + 2 and launches <= 8, (calls, launches, st)
 
 
 def test_async_and_threads_together(file200k):

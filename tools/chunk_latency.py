@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--records", type=int, default=2_600_000)
     ap.add_argument("--chunk", type=int, default=10_000)
     ap.add_argument("--threads", default="1,8,64")
+    ap.add_argument("--repeat", type=int, default=2, help="throughput legs per setting (the first grows the buffers)")
     args = ap.parse_args()
     S = pp.synth()
     sz = S.ppg_synth_fastq_size(0, args.records, 150)
@@ -45,7 +46,7 @@ def main():
         _, _, rec = pp.Core.ExtractDeflateIndex(slices[k], ix, k, device=dev, with_records=True)
         ts.append((time.perf_counter() - t) * 1e3)
     print(f"T=1: ms per call {np.median(ts):.2f} (min {min(ts):.2f})", flush=True)
-    for T in [int(x) for x in args.threads.split(",") if int(x) > 1]:
+    for T in [int(x) for x in args.threads.split(",") if int(x) > 1 for _ in range(args.repeat)]:
         nxt, lock, cnt = [0], threading.Lock(), [0]
         m = min(n, 16 * T)
 
@@ -71,7 +72,7 @@ def main():
         print(f"T={T}: {cnt[0] / sec / 1e6:.2f} M records/s, {m} chunks in {sec * 1e3:.1f} ms, "
               f"{after['launches'] - before['launches']} launches", flush=True)
     if hasattr(pp.Core, "ExtractDeflateIndexAsync"):
-        for depth in (64, 256, 1024):
+        for depth in [d for d in (64, 256, 1024) for _ in range(args.repeat)]:
             m = min(n, depth)
             t = time.perf_counter()
             futs = [pp.Core.ExtractDeflateIndexAsync(slices[k], ix, k, device=dev) for k in range(m)]

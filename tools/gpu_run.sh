@@ -24,6 +24,7 @@
 #   stamps[:args]               the PPG_STAMPS diagnostic build (abtmp/stamps) on the bench workload
 #                               (e.g. stamps:--share_8)                            -> stamps*.log
 #   chunkapi                    the per-chunk Decompress leg only ($CHUNK_ARGS)    -> chunkapi.json
+#   latency[:args]              tools/chunk_latency.py with every launch's phases  -> chunk_latency.txt
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 tag=$1; shift
@@ -98,6 +99,9 @@ run_step() {
     timeout -k 10 400 python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ingest --no-enumerate $xa \
       > $O/chunkapi.json 2> $O/chunkapi.log || return $?
     python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]); c=d.get('decompress_chunk', {}); print(json.dumps(c)[:1500])" $O/chunkapi.json ;;
+  latency)
+    PPG_CHUNK_VERBOSE=1 timeout -k 10 300 python3 -u tools/chunk_latency.py $xa > $O/chunk_latency.txt 2>&1 || { tail -5 $O/chunk_latency.txt; return 1; }
+    grep -v PPG_CHUNK $O/chunk_latency.txt | tail -14 ;;
   *)
     echo "gpu_run.sh: unknown step $step" >&2; return 2 ;;
   esac
