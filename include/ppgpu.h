@@ -154,17 +154,20 @@ int ppg_stream_wait_ctx(ppg_ctx *ctx, void *stream);
  * a chunk of an index without them gets its inner block starts found on the GPU first (candidate
  * block headers, a speculative symbolic decode, the verified chain of block ends from the chunk's
  * Point and their resolved 32 KiB histories -- CreateIndex's own kernels) and is decoded as up to
- * 16 pieces too.  Environment PPG_CHUNK_NO_FIND=1 turns the search off. */
+ * 16 pieces too; in a launch of at most 256 such chunks the search's symbolic decode covers each
+ * whole chunk and a chunk whose chain is verified end to end is written out from its symbols, with
+ * no second decode.  Environment PPG_CHUNK_NO_FIND=1 turns the search off (PPG_CHUNK_NO_MAT=1 only
+ * the write-out from symbols). */
 int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
                          uint8_t *out, int64_t out_cap, int64_t *produced, uint32_t *recs, int64_t rec_cap,
                          int64_t *nrec);
 /* The same, asynchronous: one caller keeps many chunks in flight, as the reference's reader keeps 32
  * partitions queued (LazyFileReader.cs:14) for its tasks.  submit queues the request and returns a
  * ticket at once; a launcher thread of the ctx (started by the first submit) combines the queued
- * requests -- a burst of submissions goes into one launch of up to 1,024 chunks -- and
- * ppg_decompress_chunk_wait blocks until the ticket's chunk is decoded, copies its bytes / records
- * into the buffers given at submit (slice, out and recs must stay valid until then) and frees the
- * ticket.  Every ticket must be waited for, each once, on the ctx it was submitted to. */
+ * requests -- a burst of submissions goes into one launch of up to 256 chunks --, copies each
+ * decoded chunk's bytes / records into the buffers given at submit (up to 8 threads per launch), and
+ * ppg_decompress_chunk_wait blocks until that is done, returns the status and counts, and frees the
+ * ticket (slice, out and recs must stay valid until then).  Every ticket must be waited for, each once, on the ctx it was submitted to. */
 typedef struct ppg_chunk_req ppg_chunk_req;
 int ppg_decompress_chunk_submit(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
                                 uint8_t *out, int64_t out_cap, uint32_t *recs, int64_t rec_cap, ppg_chunk_req **req);

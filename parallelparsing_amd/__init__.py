@@ -379,7 +379,7 @@ class Core:
     def ExtractDeflateIndexAsync(file_buffer, index, k, buf=None, device=None):
         """ExtractDeflateIndex queued without blocking (ppg_decompress_chunk_submit): returns a
         ChunkFuture whose result() is (produced, buf, records).  Many queued chunks share launches
-        of up to 1,024 chunks; every future's result() must be taken (it frees the ticket)."""
+        of up to 256 chunks; every future's result() must be taken (it frees the ticket)."""
         dev = device or Device.default()
         src = _as_u8(file_buffer)
         o0, _, _, _ = index.point_fields(k)

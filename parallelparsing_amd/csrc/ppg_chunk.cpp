@@ -47,7 +47,9 @@ constexpr uint64_t kPieceRing = 65536;     // CreateIndex pass 1's symbolic outp
 // waves per chunk, so 4,096 chunks already hold ~8 generations of the GPU's 8,192 wave slots
 constexpr int kFindMaxChunks = 4096;
 constexpr size_t kSliceAlign = 64;   // each gathered slice starts on its own 64-B line
-constexpr size_t kMaxBatch = 1024;         // chunks per launch
+// chunks per launch: the materialise path's limit (find_mat, kMatMaxChunks below), whose launch of
+// 256 warm chunks takes 41 ms against 63 ms for 258 on the two-decode path (r05g)
+constexpr size_t kMaxBatch = 256;
 // a second launch starts while one is decoding only with this many requests queued: otherwise the
 // queue grows during the running launch and the next one takes all of it (r04: with two slots taken
 // as soon as free, 64 callers were served ~12 at a time)
@@ -87,7 +89,7 @@ hipError_t grow_buf(B &b, size_t need) {
 }
 
 // memcpy of many (dst, src, len) spans: on the calling thread when small, else spread over up to
-// 8 threads in 1 MiB pieces -- a launch gathers up to 1,024 slices into the pinned staging buffer and
+// 8 threads in 1 MiB pieces -- a launch gathers up to 256 slices into the pinned staging buffer and
 // the async path copies up to a GiB of results into fresh caller pages (page faults included), which
 // one thread does at a few GB/s
 struct Span {
@@ -143,9 +145,10 @@ int result_spans(const ChunkReq &req, uint8_t *out, int64_t out_cap, uint32_t *r
     return PPG_OK;
 }
 
-// waves per candidate range of the block search: enough for ~4,096 waves in all (a lone chunk's 16
-// ranges are searched by 16 waves each; a launch of hundreds of chunks fills the GPU with one each)
-int find_sub(int ranges) { return std::max(1, std::min(32, 4096 / std::max(1, ranges))); }
+// waves per candidate range of the block search: enough for ~16,384 waves in all, two generations of
+// the GPU's wave slots (a lone chunk's 16 ranges are searched by 32 waves each; r05: at 4,096 waves a
+// launch of 256 chunks searched its 3,840 ranges with one wave each, 7.0 ms)
+int find_sub(int ranges) { return std::max(1, std::min(32, 16384 / std::max(1, ranges))); }
 
 // device scratch of find_side_points (grow only)
 struct FindScratch {
@@ -459,7 +462,7 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
 // census) -- no second decode; any other chunk is decoded whole, one wave, in the same launch.
 // A lone 10,000-record chunk: find ~0.5 ms + one symbolic decode of a single deflate block (~4 ms)
 // + resolve + materialise, instead of that plus a second decode of the same block.
-constexpr int kMatMaxChunks = 256;
+constexpr int kMatMaxChunks = (int)kMaxBatch;
 constexpr uint64_t kMatRatio = 10;        // symbol capacity per compressed byte of a piece (FASTQ: ~4)
 
 struct MatPiece {

@@ -1401,9 +1401,11 @@ hipError_t ppg_launch_inflate_ixf(hipStream_t s, const uint32_t *comp, uint64_t 
 
 // A piece whose pass-1 symbols and exact starting history are known is written out without a second
 // decode: symbol 0x8000 | b is the byte b, symbol i < 32768 is byte i of the history.  The bytes go
-// through the inflate kernel's own flush path -- a 1 KiB LDS ring by global output address, flushed
-// in aligned 512-B units with the fused newline census (flush_census) -- so the piece's result and
-// census region are exactly what decoding it (ppg_inflate_kernel, CEN) would have produced.
+// through the inflate kernel's own flush path -- an LDS ring by global output address, flushed in
+// aligned units with the fused newline census (flush_census) -- so the piece's result and census
+// region are exactly what decoding it (ppg_inflate_kernel, CEN) would have produced.  A unit's 32
+// symbols per lane are loaded at once, and the next unit's while this one's census runs (r05: one
+// load after another, a 4,096-piece launch took 9.9 ms, latency-bound at 4 waves per CU).
 // mi[k].prev: the census's "previous byte" (a chunk's first piece: the job's own, from the Point's
 // offset), or > 255: the history's last byte.
 template <int RB>
@@ -1413,7 +1415,7 @@ __global__ __launch_bounds__(64) void ppg_materialize_kernel(const uint16_t *__r
                                                              const PpgInflateJob *__restrict__ jobs,
                                                              uint8_t *__restrict__ out, PpgInflateResult *__restrict__ res,
                                                              int njobs, uint32_t *__restrict__ nls) {
-    constexpr uint32_t RING = 1u << RB, RM = RING - 1, UNIT = RING / 2;
+    constexpr uint32_t RING = 1u << RB, RM = RING - 1, UNIT = RING / 2, PER = UNIT / 64;
     __shared__ __attribute__((aligned(16))) uint8_t W[32768];
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
     __shared__ uint32_t cen[8];
@@ -1423,11 +1425,9 @@ __global__ __launch_bounds__(64) void ppg_materialize_kernel(const uint16_t *__r
     const PpgMatInfo M = mi[k];
     for (uint32_t i = 16u * (uint32_t)lane; i < 32768u; i += 1024u)
         *(uint4 *)&W[i] = *(const uint4 *)(wins + M.win_off + i);
-    __syncthreads();
     if (lane == 0) {
         const uint64_t d = (uint64_t)(uintptr_t)(nls + J.nl_off);
         cen[0] = 0;
-        cen[1] = (M.prev > 255u ? W[32767] : M.prev) == '\n';
         cen[2] = 0;
         cen[3] = J.nl_cap;
         cen[4] = J.raw_shift;
@@ -1435,19 +1435,35 @@ __global__ __launch_bounds__(64) void ppg_materialize_kernel(const uint16_t *__r
         cen[6] = (uint32_t)(d >> 32);
     }
     __syncthreads();
+    if (lane == 0) cen[1] = (M.prev > 255u ? W[32767] : M.prev) == '\n';
     const uint32_t len = (uint32_t)J.out_len;
     const uint64_t out_off = J.out_off;
     const uint16_t *sy = sym + M.sym_off;
-    for (uint32_t p0 = 0; p0 < len;) {
-        const uint32_t p1 = min(len, p0 + (UNIT - (uint32_t)((out_off + p0) & (UNIT - 1))));
-        for (uint32_t p = p0 + (uint32_t)lane; p < p1; p += 64) {
-            const uint32_t v = sy[p];
-            ring[(uint32_t)(out_off + p) & RM] = (uint8_t)((v & 0x8000u) ? v : W[v & 32767u]);
+    // units end at UNIT-aligned output addresses (or the piece's end)
+    auto unit_end = [&](uint32_t p) { return min(len, p + (UNIT - (uint32_t)((out_off + p) & (UNIT - 1)))); };
+    uint32_t v[PER];
+    auto fetch = [&](uint32_t p0, uint32_t p1) {
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            const uint32_t p = p0 + (uint32_t)lane + 64u * i;
+            v[i] = p < p1 ? (uint32_t)sy[p] : 0x8000u;
+        }
+    };
+    uint32_t p0 = 0, p1 = unit_end(0);
+    fetch(p0, p1);
+    while (p0 < len) {
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            const uint32_t p = p0 + (uint32_t)lane + 64u * i;
+            if (p < p1) ring[(uint32_t)(out_off + p) & RM] = (uint8_t)((v[i] & 0x8000u) ? v[i] : W[v[i] & 32767u]);
         }
         __syncthreads();
+        const uint32_t q1 = unit_end(p1);
+        fetch(p1, q1);   // (empty past the end)
         flush_census<RB>(ring, out, out_off, p0, p1, lane, cen);
         __syncthreads();
         p0 = p1;
+        p1 = q1;
     }
     if (lane == 0) {
         res[k].produced = len;
@@ -1465,6 +1481,6 @@ hipError_t ppg_launch_materialize(hipStream_t s, const uint16_t *sym, const uint
                                   const PpgInflateJob *jobs, uint8_t *out, PpgInflateResult *res, int njobs,
                                   uint32_t *nls) {
     if (njobs <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ppg_materialize_kernel<10>, dim3(njobs), dim3(64), 0, s, sym, wins, mi, jobs, out, res, njobs, nls);
+    hipLaunchKernelGGL(ppg_materialize_kernel<12>, dim3(njobs), dim3(64), 0, s, sym, wins, mi, jobs, out, res, njobs, nls);
     return hipGetLastError();
 }
