@@ -427,9 +427,11 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
         return {"chunks": n, "records_per_s": float(got.sum()) / sec, "chunks_per_s": n / sec, "seconds": sec,
                 "launches": after["launches"] - before["launches"]}
 
-    leg(plain, 8)   # warm: the slots' buffers grow to their working size
+    # warm: the launcher thread, and every launch slot's buffers grown to a full launch (256 chunks
+    # each; r05: warming one slot left depth 1024 at 16.5 M records/s against 30.4 for depth 256)
+    async_leg(plain, nmax)
+    leg(plain, 8)
     out = {f"T{T}": leg(plain, T) for T in threads_list}
-    async_leg(plain, 256)   # warm the launcher thread and the larger launches' buffers
     out["async"] = {f"depth{d}": async_leg(plain, d) for d in (256, 1024)}
     out["no_find"] = {f"T{T}": no_find(T) for T in threads_list}
     out["side_points"] = {f"T{T}": leg(split, T) for T in threads_list}
