@@ -579,6 +579,15 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
     emit_ms = []
 
     def step(emit=True):
+        if emit and world == 1:
+            # one rank: the emission drives the shards' own run (ppg_pairs_emit_run): each output
+            # batch of both files decoded once and its pair chunk halves packed while it is
+            # resident, then the check over the keys the batches wrote
+            t = time.perf_counter()
+            for _ in pairs.emit_run(shards[0], shards[1], K, window_bytes=int(args.pair_window_gib * (1 << 30))):
+                pass
+            emit_ms.append((time.perf_counter() - t) * 1e3)
+            return paired.require_pairs(pairs.check(shards[0], shards[1]))
         errs = []
 
         def run(sh):
@@ -633,8 +642,11 @@ def paired_run(args, dev, world=1, rank=0, xdev=None, backend="nccl"):
                 "batches_rerun_per_step": est["reruns"],
                 "verified": verify_pair_chunks(pairs, tfs, K, shards, comm, world, rank),
                 "note": "every pair chunk of this rank packed on the device per step (records back to back + "
-                        "descriptors per half, ppg_pairs_emit_*), inside the timed step; multi-batch shards on one "
-                        "GPU run their batches again as the windows advance"}
+                        "descriptors per half, ppg_pairs_emit_*), inside the timed step; one rank: the emission "
+                        "drives the shards' own run (ppg_pairs_emit_run: each output batch decoded once, its "
+                        "halves packed while resident; ms_per_step = decode + packing, rerun_ms = the batches' "
+                        "runs), the pair check after it; N ranks: decode, check, then the records moved to "
+                        "their pair chunk's owner"}
     # the previous round's line (decode + check, no emission) for comparison, timed after the main loop
     t1 = time.perf_counter()
     for _ in range(args.steps):
@@ -678,7 +690,8 @@ def verify_pair_chunks(pairs, tfs, K, shards, comm, world, rank, samples=3):
     one, the last -- copied to the host, each half's bytes and descriptors equal to records
     [j*K, (j+1)*K) of its member (pair i = record i mod the segment's records of both files)."""
     want = set()
-    for j0, j1 in pairs.emit(shards[0], shards[1], K, comm):
+    it = pairs.emit_run(shards[0], shards[1], K) if world == 1 else pairs.emit(shards[0], shards[1], K, comm)
+    for j0, j1 in it:
         span = list(range(j0, j1))
         pick = {span[0], span[-1], span[len(span) // 2]} if span else set()
         for j in sorted(pick)[:samples]:

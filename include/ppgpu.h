@@ -386,17 +386,25 @@ void ppg_pairs_free(ppg_pairs *p);
  *      and a pair chunk that straddles a batch boundary is carried across; nothing else may run the
  *      shards until the emission is done.  N ranks: rank r owns the pair chunks that start in its
  *      R1 range; the shards must be one-batch (resident; else PPG_UNSUPPORTED).
+ *  ppg_pairs_emit_run    one rank, no check first: the emission drives the shards' own run.  Both
+ *      shards carry a keys buffer (ppg_shard_set_keys); their batches run once each, in order, as
+ *      the windows advance -- each batch's records numbered (its Q1 duplicates found from its keys)
+ *      and packed while it is resident, so a multi-batch shard is decoded once, not twice.  After
+ *      the last window (PPG_STREAM_END) both shards stand as ppg_shard_run leaves them and
+ *      ppg_pairs_check follows (it may report mismatches the windows already emitted).  A caller
+ *      that stops early leaves the shards unrun.
  *  ppg_pairs_emit_next   packs the next window of this rank's pair chunks [*j0, *j1) on the device;
  *      PPG_STREAM_END when there is none.  N ranks: the first call is collective (every rank calls
  *      it: the records a rank does not hold move from their ranks over ppg_comm_alltoallv -- RCCL
  *      ncclSend / ncclRecv over xGMI, or the host transport) and is the rank's one window.
  *  ppg_pairs_chunk       device pointers of a half of the current window (valid until the next call).
  *  ppg_pairs_copy_chunk  a half into caller memory (bytes and/or descriptors; NULL skips).
- *  ppg_pairs_emit_stats  [0] ms re-running batches, [1] ms packing, [2] ms exchanging, [3] ms in
+ *  ppg_pairs_emit_stats  [0] ms (re-)running batches, [1] ms packing, [2] ms exchanging, [3] ms in
  *      emit_next, [4] batches re-run, [5] pair chunks in all, [6..7] this rank's [j_lo, j_hi)
- *      (N ranks: after the exchange). */
+ *      (N ranks: after the exchange; emit_run: [5] and [7] once the last window is out). */
 int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *comm, int64_t pair_chunk,
                          int64_t window_bytes);
+int ppg_pairs_emit_run(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, int64_t pair_chunk, int64_t window_bytes);
 int ppg_pairs_emit_next(ppg_pairs *p, int64_t *j0, int64_t *j1);
 int ppg_pairs_chunk(ppg_pairs *p, int64_t j, int32_t file, const uint8_t **bytes, int64_t *len, const uint32_t **desc,
                     int64_t *nrec);

@@ -169,6 +169,8 @@ internal static unsafe class PpGpu
     // record-aligned pair chunks, packed on the device (ppg_pairs_emit_*)
     [DllImport(Lib)] public static extern int ppg_pairs_emit_begin(nint pairs, nint r1, nint r2, nint comm,
         long pairChunk, long windowBytes);
+    [DllImport(Lib)] public static extern int ppg_pairs_emit_run(nint pairs, nint r1, nint r2, long pairChunk,
+        long windowBytes);
     [DllImport(Lib)] public static extern int ppg_pairs_emit_next(nint pairs, out long j0, out long j1);
     [DllImport(Lib)] public static extern int ppg_pairs_chunk(nint pairs, long j, int file, out nint bytes, out long len,
         out nint desc, out long nrec);

@@ -133,6 +133,7 @@ _SIGS = {
     "ppg_pairs_records": (C.c_int, [vp, i32, i64, i64, vp]),
     "ppg_pairs_free": (None, [vp]),
     "ppg_pairs_emit_begin": (C.c_int, [vp, vp, vp, vp, i64, i64]),
+    "ppg_pairs_emit_run": (C.c_int, [vp, vp, vp, i64, i64]),
     "ppg_pairs_emit_next": (C.c_int, [vp, P(i64), P(i64)]),
     "ppg_pairs_chunk": (C.c_int, [vp, i64, i32, P(vp), P(i64), P(vp), P(i64)]),
     "ppg_pairs_copy_chunk": (C.c_int, [vp, i64, i32, vp, i64, P(i64), vp, i64, P(i64)]),

@@ -190,7 +190,11 @@ struct PairEmit {
     // N ranks: exchange buffers (bytes as int64 words, descriptors as two int64 per record)
     DevBuf<int64_t> sbuf[2], rbuf[2], sdesc[2], rdesc[2];
     RerunSave save[2];
-    double t_ms[4] = {0, 0, 0, 0};          // batches re-run, packing, exchange, total (ms, cumulative)
+    // fused (ppg_pairs_emit_run): the shards' own first run, batch by batch as the windows advance
+    bool fused = false;
+    bool done[2] = {false, false};          // the file's last batch has run (shard finished)
+    float run_ms[2] = {0, 0};               // its batches' kernel time, as shard_run sums it
+    double t_ms[4] = {0, 0, 0, 0};          // batches (re-)run, packing, exchange, total (ms, cumulative)
     int64_t reruns = 0;
     void release() {
         for (int f = 0; f < 2; f++) {
@@ -538,75 +542,12 @@ int rerun_collect(ppg_shard *sh, int32_t b, const RerunSave &sv) {
     return rc;
 }
 
-// ---- one rank: windows over the shards' batches ----
-int emit_next_local(ppg_pairs *p, int64_t *j0, int64_t *j1) {
+// Steps 2-3 of a one-rank window: pair chunks [e, J) are complete in both files' resident batches
+// (pairs: the pair count, or a bound below which every pair chunk < J is final); the window is cut
+// at the byte budget, then both files' halves are placed and packed
+int pack_window(ppg_pairs *p, int64_t e, int64_t J, int64_t pairs, Clock::time_point t0, int64_t *j0, int64_t *j1) {
     PairEmit &E = p->em;
-    const int64_t K = E.K, pairs = p->res.pairs, e = E.next;
-    if (e >= E.j_hi) return PPG_STREAM_END;
-    const auto t0 = Clock::now();
-    // 1. each file's resident batch must complete pair chunk e; a batch holding only its first part
-    //    hands that part to the carry first (the next batch's run overwrites the output).  Both
-    //    files' batches run together, each on its shard's own stream.
-    const int64_t need = std::min((e + 1) * K, pairs);
-    for (;;) {
-        bool run[2] = {false, false};
-        for (int f = 0; f < 2; f++) {
-            ppg_shard *sh = E.sh[f];
-            const int64_t cend = e * K + E.cnrec[f];
-            const int32_t b = E.batch[f];
-            if (E.blo[f][(size_t)b] <= cend && E.bhi[f][(size_t)b] >= need) continue;
-            hipStream_t s = shard_stream(sh);
-            if (E.blo[f][(size_t)b] <= cend && cend < E.bhi[f][(size_t)b]) {
-                std::vector<PpgPackSeg> seg;
-                std::vector<SegPlace> pl;
-                make_segs(p, f, cend, E.bhi[f][(size_t)b], 0, seg, pl);
-                if (int rc = seg_bounds(E, seg, s)) return rc;
-                int64_t add = 0, nadd = 0;
-                for (auto &g : seg) {
-                    g.dst = (uint64_t)(E.clen[f] + add);
-                    g.ddst = (uint64_t)(E.cnrec[f] + nadd);
-                    g.delta = (int64_t)g.dst - (int64_t)g.a;   // the carry starts its half
-                    add += (int64_t)(g.b - g.a);
-                    nadd += g.nrec;
-                }
-                if (int rc = grow_keep(E.cbytes[f], (size_t)(E.clen[f] + add) + 64, s, (size_t)E.clen[f])) return rc;
-                if (int rc = grow_keep(E.cdesc[f], 4 * (size_t)(E.cnrec[f] + nadd) + 4, s, 4 * (size_t)E.cnrec[f])) return rc;
-                if (int rc = seg_pack(E, seg, E.cbytes[f].p, E.cdesc[f].p, s)) return rc;
-                E.clen[f] += add;
-                E.cnrec[f] += nadd;
-            }
-            // the batch holding the carry's end
-            const int64_t c2 = e * K + E.cnrec[f];
-            int32_t nb = 0;
-            while ((size_t)nb + 1 < E.bhi[f].size() && E.bhi[f][(size_t)nb] <= c2) nb++;
-            if (nb == b) return PPG_DATA_ERROR;   // no progress: the batches cannot complete the pair chunk
-            E.batch[f] = nb;
-            run[f] = true;
-        }
-        if (!run[0] && !run[1]) break;
-        const auto tr = Clock::now();
-        int rc = PPG_OK;
-        bool launched[2] = {false, false};
-        for (int f = 0; f < 2 && rc == PPG_OK; f++)
-            if (run[f]) {
-                rc = rerun_launch(E.sh[f], E.batch[f], E.save[f]);
-                launched[f] = rc == PPG_OK;
-            }
-        for (int f = 0; f < 2; f++)
-            if (launched[f]) {
-                const int x = rerun_collect(E.sh[f], E.batch[f], E.save[f]);
-                if (rc == PPG_OK) rc = x;
-            }
-        if (rc != PPG_OK) return rc;
-        E.reruns += run[0] + run[1];
-        E.t_ms[0] += ms_since(tr);
-    }
-    // 2. the window: the pair chunks both resident batches complete, within the byte budget
-    int64_t J = E.j_hi;
-    for (int f = 0; f < 2; f++) {
-        const int64_t hi = E.bhi[f][(size_t)E.batch[f]];
-        if (hi < pairs) J = std::min(J, hi / K);
-    }
+    const int64_t K = E.K;
     if (J <= e) return PPG_DATA_ERROR;
     const auto tp = Clock::now();
     std::vector<PpgPackSeg> seg[2];
@@ -687,6 +628,211 @@ int emit_next_local(ppg_pairs *p, int64_t *j0, int64_t *j1) {
     if (j0) *j0 = e;
     if (j1) *j1 = J2;
     return PPG_OK;
+}
+
+// A resident batch b holding only the first part of the current pair chunk's half (records from
+// cend on): that part goes to the carry before the next batch's run overwrites the output
+int carry_rest(ppg_pairs *p, int f, int64_t cend, int32_t b) {
+    PairEmit &E = p->em;
+    if (b < 0 || !(E.blo[f][(size_t)b] <= cend && cend < E.bhi[f][(size_t)b])) return PPG_OK;
+    hipStream_t s = shard_stream(E.sh[f]);
+    std::vector<PpgPackSeg> seg;
+    std::vector<SegPlace> pl;
+    make_segs(p, f, cend, E.bhi[f][(size_t)b], 0, seg, pl);
+    if (int rc = seg_bounds(E, seg, s)) return rc;
+    int64_t add = 0, nadd = 0;
+    for (auto &g : seg) {
+        g.dst = (uint64_t)(E.clen[f] + add);
+        g.ddst = (uint64_t)(E.cnrec[f] + nadd);
+        g.delta = (int64_t)g.dst - (int64_t)g.a;   // the carry starts its half
+        add += (int64_t)(g.b - g.a);
+        nadd += g.nrec;
+    }
+    if (int rc = grow_keep(E.cbytes[f], (size_t)(E.clen[f] + add) + 64, s, (size_t)E.clen[f])) return rc;
+    if (int rc = grow_keep(E.cdesc[f], 4 * (size_t)(E.cnrec[f] + nadd) + 4, s, 4 * (size_t)E.cnrec[f])) return rc;
+    if (int rc = seg_pack(E, seg, E.cbytes[f].p, E.cdesc[f].p, s)) return rc;
+    E.clen[f] += add;
+    E.cnrec[f] += nadd;
+    return PPG_OK;
+}
+
+// ---- one rank: windows over the shards' batches ----
+int emit_next_local(ppg_pairs *p, int64_t *j0, int64_t *j1) {
+    PairEmit &E = p->em;
+    const int64_t K = E.K, pairs = p->res.pairs, e = E.next;
+    if (e >= E.j_hi) return PPG_STREAM_END;
+    const auto t0 = Clock::now();
+    // 1. each file's resident batch must complete pair chunk e; a batch holding only its first part
+    //    hands that part to the carry first (the next batch's run overwrites the output).  Both
+    //    files' batches run together, each on its shard's own stream.
+    const int64_t need = std::min((e + 1) * K, pairs);
+    for (;;) {
+        bool run[2] = {false, false};
+        for (int f = 0; f < 2; f++) {
+            ppg_shard *sh = E.sh[f];
+            const int64_t cend = e * K + E.cnrec[f];
+            const int32_t b = E.batch[f];
+            if (E.blo[f][(size_t)b] <= cend && E.bhi[f][(size_t)b] >= need) continue;
+            if (int rc = carry_rest(p, f, cend, b)) return rc;
+            (void)sh;
+            // the batch holding the carry's end
+            const int64_t c2 = e * K + E.cnrec[f];
+            int32_t nb = 0;
+            while ((size_t)nb + 1 < E.bhi[f].size() && E.bhi[f][(size_t)nb] <= c2) nb++;
+            if (nb == b) return PPG_DATA_ERROR;   // no progress: the batches cannot complete the pair chunk
+            E.batch[f] = nb;
+            run[f] = true;
+        }
+        if (!run[0] && !run[1]) break;
+        const auto tr = Clock::now();
+        int rc = PPG_OK;
+        bool launched[2] = {false, false};
+        for (int f = 0; f < 2 && rc == PPG_OK; f++)
+            if (run[f]) {
+                rc = rerun_launch(E.sh[f], E.batch[f], E.save[f]);
+                launched[f] = rc == PPG_OK;
+            }
+        for (int f = 0; f < 2; f++)
+            if (launched[f]) {
+                const int x = rerun_collect(E.sh[f], E.batch[f], E.save[f]);
+                if (rc == PPG_OK) rc = x;
+            }
+        if (rc != PPG_OK) return rc;
+        E.reruns += run[0] + run[1];
+        E.t_ms[0] += ms_since(tr);
+    }
+    // 2. the window: the pair chunks both resident batches complete, within the byte budget
+    int64_t J = E.j_hi;
+    for (int f = 0; f < 2; f++) {
+        const int64_t hi = E.bhi[f][(size_t)E.batch[f]];
+        if (hi < pairs) J = std::min(J, hi / K);
+    }
+    return pack_window(p, e, J, pairs, t0, j0, j1);
+}
+
+// ---- one rank, fused (ppg_pairs_emit_run): the shards' first run, driven by the windows ----
+// Batch b of file f has just run for the first time: its chunks' parse info, the duplicates among
+// its records (ppg_key_dups over its keys; SURVEY Q1: at most one per chunk, so the numbering map
+// grows batch by batch), its deduplicated record range; after the file's last batch the shard is
+// finished exactly as ppg_shard_run leaves it (results, status, keys marked written).
+int fused_collected(ppg_pairs *p, int f, int32_t b) {
+    PairEmit &E = p->em;
+    ppg_shard *sh = E.sh[f];
+    hipStream_t s = shard_stream(sh);
+    const auto [b0, b1] = sh->batches[(size_t)b];
+    const int64_t r0 = sh->h_base[(size_t)b0], r1 = sh->total_records;
+    sh->h_info.resize((size_t)sh->n);
+    if (b1 > b0)
+        HIPCHK(hipMemcpyAsync(sh->h_info.data() + b0, sh->info.p + b0, sizeof(PpgParseInfo) * (size_t)(b1 - b0),
+                              hipMemcpyDeviceToHost, s));
+    const uint32_t cap = (uint32_t)(b1 - b0) + 16;
+    HIPCHK(grow(p->dpos, cap));
+    HIPCHK(grow(p->dcount, 1));
+    HIPCHK(hipMemsetAsync(p->dcount.p, 0, 4, s));
+    if (r1 > r0)
+        hipLaunchKernelGGL(ppg_key_dups, dim3(grid_for((uint64_t)(r1 - r0))), dim3(256), 0, s, sh->keys_dev + r0,
+                           (uint64_t)(r1 - r0), p->dpos.p, cap, p->dcount.p);
+    HIPCHK(hipGetLastError());
+    uint32_t nd = 0;
+    HIPCHK(hipMemcpyAsync(&nd, p->dcount.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nd > cap) return PPG_DATA_ERROR;
+    std::vector<uint64_t> pos(nd);
+    if (nd) HIPCHK(hipMemcpy(pos.data(), p->dpos.p, 8 * (size_t)nd, hipMemcpyDeviceToHost));
+    std::sort(pos.begin(), pos.end());
+    for (uint64_t x : pos) {
+        const int64_t r = r0 + (int64_t)x;
+        p->dp[f].push_back(r - (int64_t)E.pos[f].size());
+        E.pos[f].push_back(r);
+    }
+    E.blo[f].push_back(dedup_of(E.pos[f], r0));
+    E.bhi[f].push_back(dedup_of(E.pos[f], r1));
+    if ((size_t)b + 1 == sh->batches.size()) {
+        const int rc = shard_finish(sh, E.run_ms[f]);
+        sh->last_rc = rc;
+        sh->keys_written = rc == PPG_OK && sh->keys_dev != nullptr;
+        if (rc != PPG_OK) return rc;
+        E.done[f] = true;
+        p->local[f] = sh->total_records - (int64_t)E.pos[f].size();
+    }
+    return PPG_OK;
+}
+
+// the next batch of the files in run[] (first runs, both in flight together)
+int fused_run(ppg_pairs *p, const bool run[2]) {
+    PairEmit &E = p->em;
+    const auto tr = Clock::now();
+    int rc = PPG_OK;
+    bool launched[2] = {false, false};
+    for (int f = 0; f < 2 && rc == PPG_OK; f++)
+        if (run[f]) {
+            ppg_shard *sh = E.sh[f];
+            const int32_t b = ++E.batch[f];
+            rc = batch_launch(sh, sh->batches[(size_t)b].first, sh->batches[(size_t)b].second);
+            launched[f] = rc == PPG_OK;
+        }
+    for (int f = 0; f < 2; f++)
+        if (launched[f]) {
+            ppg_shard *sh = E.sh[f];
+            const int32_t b = E.batch[f];
+            int x = batch_collect(sh, sh->batches[(size_t)b].first, sh->batches[(size_t)b].second, E.run_ms[f]);
+            if (x == PPG_OK) x = fused_collected(p, f, b);
+            if (x != PPG_OK) sh->last_rc = x;
+            if (rc == PPG_OK) rc = x;
+        }
+    E.t_ms[0] += ms_since(tr);
+    return rc;
+}
+
+// pairs known so far: the smaller finished file's deduplicated count bounds them (INT64_MAX: neither)
+int64_t fused_bound(const ppg_pairs *p) {
+    int64_t b = INT64_MAX;
+    for (int f = 0; f < 2; f++)
+        if (p->em.done[f]) b = std::min(b, p->local[f]);
+    return b;
+}
+
+int emit_next_fused(ppg_pairs *p, int64_t *j0, int64_t *j1) {
+    PairEmit &E = p->em;
+    const int64_t K = E.K, e = E.next;
+    const auto t0 = Clock::now();
+    for (;;) {
+        const int64_t bound = fused_bound(p);
+        if (bound != INT64_MAX && e * K >= bound) {
+            // no pair chunk left: the unfinished file's remaining batches still run (the shards end
+            // as ppg_shard_run leaves them, for ppg_pairs_check and the shards' own results)
+            for (int f = 0; f < 2; f++)
+                while (!E.done[f]) {
+                    const bool run[2] = {f == 0, f == 1};
+                    if (int rc = fused_run(p, run)) return rc;
+                }
+            E.npc = (std::min(p->local[0], p->local[1]) + K - 1) / K;
+            E.j_hi = E.npc;
+            return PPG_STREAM_END;
+        }
+        // 1. each file's resident batch must complete pair chunk e (the first part carried over when
+        //    the batch holds only that); else its next batch runs
+        const int64_t need = std::min((e + 1) * K, bound);
+        bool run[2] = {false, false};
+        for (int f = 0; f < 2; f++) {
+            const int64_t cend = e * K + E.cnrec[f];
+            const int32_t b = E.batch[f];
+            if (b >= 0 && E.blo[f][(size_t)b] <= cend && E.bhi[f][(size_t)b] >= need) continue;
+            if (E.done[f]) return PPG_DATA_ERROR;   // every batch has run and the pair chunk is not complete
+            if (int rc = carry_rest(p, f, cend, b)) return rc;
+            run[f] = true;
+        }
+        if (!run[0] && !run[1]) break;
+        if (int rc = fused_run(p, run)) return rc;
+    }
+    // 2. the window: what both resident batches complete (a finished file's last batch reaches its
+    //    end; the pair count is final once both have finished, bounded by a finished file's before)
+    const int64_t bound = fused_bound(p);
+    int64_t J = bound == INT64_MAX ? INT64_MAX : (bound + K - 1) / K;
+    for (int f = 0; f < 2; f++)
+        if (!(E.done[f] && (size_t)E.batch[f] + 1 == E.sh[f]->batches.size()))
+            J = std::min(J, E.bhi[f][(size_t)E.batch[f]] / K);
+    return pack_window(p, e, J, bound, t0, j0, j1);
 }
 
 // ---- N ranks: one window, the records this rank does not hold moved over the comm ----
@@ -971,6 +1117,7 @@ int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *c
     E.window_bytes = window_bytes > 0 ? window_bytes : (int64_t)8 << 30;
     E.clen[0] = E.clen[1] = E.cnrec[0] = E.cnrec[1] = 0;
     E.reruns = 0;
+    E.fused = false;
     for (double &t : E.t_ms) t = 0;
     for (int f = 0; f < 2; f++) {
         ppg_shard *sh = E.sh[f];
@@ -1008,10 +1155,71 @@ int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *c
     return PPG_OK;
 }
 
+int ppg_pairs_emit_run(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, int64_t pair_chunk, int64_t window_bytes) {
+    if (!p || !r1 || !r2 || pair_chunk < 1 || r1 == r2 || r1->ctx->device != r2->ctx->device) return PPG_ARG_ERROR;
+    if (!r1->keys_dev || !r2->keys_dev) return PPG_ARG_ERROR;   // the numbering needs each batch's spot keys
+    if (p->device != r1->ctx->device) {
+        if (p->device >= 0) {
+            (void)hipSetDevice(p->device);
+            p->release();
+        }
+        p->device = r1->ctx->device;
+    }
+    HIPCHK(hipSetDevice(p->device));
+    p->checked = false;
+    p->res = ppg_pair_result{};
+    p->rank = 0;
+    p->nranks = 1;
+    p->start[0] = p->start[1] = 0;
+    PairEmit &E = p->em;
+    E.on = false;
+    E.fused = true;
+    E.K = pair_chunk;
+    E.npc = INT64_MAX;   // known once both files have run
+    E.sh[0] = r1;
+    E.sh[1] = r2;
+    E.comm = nullptr;
+    E.exchanged = false;
+    E.next = E.w0 = E.w1 = 0;
+    E.window_bytes = window_bytes > 0 ? window_bytes : (int64_t)8 << 30;
+    E.reruns = 0;
+    for (double &t : E.t_ms) t = 0;
+    E.j_lo = 0;
+    E.j_hi = INT64_MAX;
+    for (int f = 0; f < 2; f++) {
+        ppg_shard *sh = E.sh[f];
+        shard_reset(sh);
+        sh->keys_written = 0;
+        sh->last_rc = PPG_OK;
+        E.clen[f] = E.cnrec[f] = 0;
+        E.done[f] = false;
+        E.run_ms[f] = 0;
+        E.batch[f] = -1;
+        E.blo[f].clear();
+        E.bhi[f].clear();
+        E.pos[f].clear();
+        p->dp[f].clear();
+        p->local[f] = 0;
+        E.offst[f].assign((size_t)sh->n, 0);
+        uint64_t o = 0;
+        for (int32_t k = 0; k < sh->n; k++) {
+            E.offst[f][(size_t)k] = o;
+            o += sh->h_jobs[(size_t)k].raw_shift;
+        }
+    }
+    E.on = true;
+    return PPG_OK;
+}
+
 int ppg_pairs_emit_next(ppg_pairs *p, int64_t *j0, int64_t *j1) {
     if (!p || !p->em.on) return PPG_ARG_ERROR;
     HIPCHK(hipSetDevice(p->device));
     PairEmit &E = p->em;
+    if (E.fused) {
+        const int rc = emit_next_fused(p, j0, j1);
+        if (rc < 0) E.on = false;
+        return rc;
+    }
     if (p->nranks > 1) {
         if (E.exchanged) return PPG_STREAM_END;
         const int rc = emit_exchange(p, j0, j1);

@@ -99,6 +99,24 @@ class Pairs:
             check(rc, "ppg_pairs_emit_next")
             yield j0.value, j1.value
 
+    def emit_run(self, r1, r2, pair_chunk, window_bytes=0):
+        """The same windows with no check first, the emission driving the shards' own run
+        (ppg_pairs_emit_run): each output batch of both shards decoded once and its records packed
+        while resident.  Both shards need attach_keys; after the last window both have run (as
+        Shard.run leaves them) and check() may follow."""
+        for r in (r1, r2):
+            if r._on_device:
+                r._torch_order()   # the caller may have rewritten comp since the last run
+        check(lib.ppg_pairs_emit_run(self._h, r1.handle, r2.handle, int(pair_chunk), int(window_bytes)),
+              "ppg_pairs_emit_run")
+        j0, j1 = C.c_int64(), C.c_int64()
+        while True:
+            rc = lib.ppg_pairs_emit_next(self._h, C.byref(j0), C.byref(j1))
+            if rc == 1:   # PPG_STREAM_END
+                return
+            check(rc, "ppg_pairs_emit_next")
+            yield j0.value, j1.value
+
     def chunk(self, j, f):
         """(device address of the bytes, length, device address of the descriptors, records) of
         file f's half of pair chunk j (current window)."""

@@ -107,26 +107,37 @@ def test_configs4_full_size_pair_on_one_gpu(device):
     pairs = 2_621_440 * reps
     pr = paired.Pairs()
     pr.check(shards[0], shards[1])
-    nbytes, nxt, windows = [0, 0], 0, 0
-    for j0, j1 in pr.emit(shards[0], shards[1], K, window_bytes=8 << 30):
-        assert j0 == nxt
-        for j in range(j0, j1):
-            for f in (0, 1):
-                _, n, _, r = pr.chunk(j, f)
-                assert r == min(K, pairs - j * K), (j, f, r)
-                nbytes[f] += n
-            if j == j0 or j == -(-pairs // K) - 1:
-                for f, tf in enumerate(tfs):
-                    b, d = pr.copy_chunk(j, f)
-                    eb = _records_text(tf, j * K, min((j + 1) * K, pairs))
-                    assert b.tobytes() == eb, (j, f)
-                    nl = np.nonzero(np.frombuffer(eb, np.uint8) == 10)[0].astype(np.uint32).reshape(-1, 4)
-                    assert np.array_equal(d, nl), (j, f)
-        nxt = j1
-        windows += 1
-    assert nxt == -(-pairs // K) and windows > 10
-    assert nbytes == [int(tf.p_output[-1]) for tf in tfs]
+
+    def check_windows(it):
+        nbytes, nxt, windows = [0, 0], 0, 0
+        for j0, j1 in it:
+            assert j0 == nxt
+            for j in range(j0, j1):
+                for f in (0, 1):
+                    _, n, _, r = pr.chunk(j, f)
+                    assert r == min(K, pairs - j * K), (j, f, r)
+                    nbytes[f] += n
+                if j == j0 or j == -(-pairs // K) - 1:
+                    for f, tf in enumerate(tfs):
+                        b, d = pr.copy_chunk(j, f)
+                        eb = _records_text(tf, j * K, min((j + 1) * K, pairs))
+                        assert b.tobytes() == eb, (j, f)
+                        nl = np.nonzero(np.frombuffer(eb, np.uint8) == 10)[0].astype(np.uint32).reshape(-1, 4)
+                        assert np.array_equal(d, nl), (j, f)
+            nxt = j1
+            windows += 1
+        assert nxt == -(-pairs // K) and windows > 10
+        assert nbytes == [int(tf.p_output[-1]) for tf in tfs]
+
+    check_windows(pr.emit(shards[0], shards[1], K, window_bytes=8 << 30))
     assert pr.emit_stats()["reruns"] >= shards[0].batches + shards[1].batches
+    # fused (ppg_pairs_emit_run, r05): the windows drive the shards' own run -- each 40 GiB batch
+    # decoded once, no re-run -- and the check after it agrees
+    check_windows(pr.emit_run(shards[0], shards[1], K, window_bytes=8 << 30))
+    assert pr.emit_stats()["reruns"] == 0
+    res2 = pr.check(shards[0], shards[1])
+    assert res2["pairs"] == pairs and res2["mismatches"] == 0 and res2["duplicates"] == res["duplicates"], res2
+    assert [sh.total_records for sh in shards] == [tf.expected_records() for tf in tfs]
 
 
 _STARTS = {}

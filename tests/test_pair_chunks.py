@@ -139,6 +139,52 @@ def test_pair_chunks_one_rank(pair_files, device, K, cap, window):
     assert seen2 == seen
 
 
+@pytest.mark.parametrize("K,cap,window,short", [(4000, 0, 0, 0), (2500, 3 << 20, 0, 0), (7777, 2 << 20, 3 << 20, 0),
+                                                (3000, 2 << 20, 0, 1234)])
+def test_pair_chunks_fused_run(pair_files, device, K, cap, window, short):
+    """ppg_pairs_emit_run: no check first -- the windows drive the shards' own (first) run, each
+    output batch decoded once and packed while resident (no batch re-run), the Q1 numbering built
+    batch by batch from the keys.  Every half equals the oracle's records; afterwards both shards
+    stand as Shard.run leaves them (same record counts) and the check agrees.  short > 0: R2 has
+    that many records fewer, so the pair count is only known once R2 has run."""
+    gz, chunks, recs, nrec = pair_files
+    if short:
+        g2 = mate_gz(2, nrec - short, 1)
+        r2, d2 = oracle_records(g2, chunks[1])
+        gz = [gz[0], g2]
+        recs = [recs[0], (r2, d2)]
+    npairs = nrec - short
+    ix = [pp.Core.BuildDeflateIndex(g, c) for g, c in zip(gz, chunks)]
+    sh = []
+    for g, i in zip(gz, ix):
+        _, i0, _, _ = i.point_fields(0)
+        _, i1, _, _ = i.point_fields(i.Count - 1)
+        s_ = pp.Shard(i, np.frombuffer(g[i0 - 1:i1], np.uint8), 0, i.Count - 1, device=device, out_capacity=cap)
+        paired.attach_keys(s_, 400_000)
+        sh.append(s_)
+    if cap:
+        assert sh[0].batches >= 3 and sh[1].batches >= 3
+    pr = paired.Pairs()
+    seen = set()
+    windows = 0
+    for j0, j1 in pr.emit_run(sh[0], sh[1], K, window_bytes=window):
+        check_window(pr, j0, j1, K, recs, npairs, seen)
+        windows += 1
+    assert seen == set(range(-(-npairs // K)))
+    st = pr.emit_stats()
+    assert st["reruns"] == 0 and st["pair_chunks"] == len(seen), st
+    if cap:
+        assert windows > 1, st
+    res = pr.check(sh[0], sh[1])
+    assert res["pairs"] == npairs and res["mismatches"] == short and res["duplicates"][0] == recs[0][1]
+    assert res["records"] == (nrec, nrec - short)
+    # the shards' own results: as a plain run leaves them
+    for s_, g, i in zip(sh, gz, ix):
+        ref = shard_of(g, i, device, cap)
+        assert s_.total_records == ref.total_records
+        assert np.array_equal(s_.results()["records"], ref.results()["records"])
+
+
 def test_paired_fastq_surface(pair_files, device, tmp_path):
     """PairedFASTQ (Python mirror of the C# GpuPairedFASTQ) over .gz files: pair chunks from the
     library's emission, the pairs' identifiers those of the oracle's records."""
