@@ -175,6 +175,7 @@ struct PairEmit {
     ppg_comm *comm = nullptr;
     bool exchanged = false;                 // N ranks: the one window is done
     int32_t batch[2] = {-1, -1};            // one rank: the resident output batch of each shard
+    int32_t kvalid[2] = {0, 0};             // chunks [0, kvalid) have their record bases (h_base) set
     std::vector<int64_t> blo[2], bhi[2];    // one rank: each batch's deduplicated record range
     std::vector<uint64_t> offst[2];         // chunk k's offset carry in sh->offs
     std::vector<int64_t> pos[2];            // shard positions of the duplicates (sorted)
@@ -447,20 +448,26 @@ struct SegPlace {
 
 // The runs of consecutive records of this rank's deduplicated records [d0, d1) of file f, split at
 // chunk boundaries and at the duplicates, from the shard's resident output batch
-void make_segs(const ppg_pairs *p, int f, int64_t d0, int64_t d1, int32_t grp, std::vector<PpgPackSeg> &seg,
+// (false: the records are not where the shard's run put them -- never expected; the caller fails
+// with PPG_DATA_ERROR instead of looping)
+bool make_segs(const ppg_pairs *p, int f, int64_t d0, int64_t d1, int32_t grp, std::vector<PpgPackSeg> &seg,
                std::vector<SegPlace> &pl) {
     const PairEmit &E = p->em;
     const ppg_shard *sh = E.sh[f];
     const auto &B = sh->h_base;
+    // chunks whose record bases are set (emit_run: the batches run so far; the rest are still 0)
+    const auto Bend = B.begin() + std::min<std::ptrdiff_t>((std::ptrdiff_t)B.size(), E.kvalid[f]);
     const auto &pos = E.pos[f];
     int64_t d = d0;
     while (d < d1) {
         const int64_t r = shard_rec(p->dp[f], d);
-        const int32_t k = (int32_t)(std::upper_bound(B.begin(), B.end(), r) - B.begin()) - 1;
+        const int32_t k = (int32_t)(std::upper_bound(B.begin(), Bend, r) - B.begin()) - 1;
+        if (k < 0) return false;
         const int64_t cend = B[(size_t)k] + (int64_t)sh->h_info[(size_t)k].records;
         const auto nd = std::upper_bound(pos.begin(), pos.end(), r);
         const int64_t stop = std::min<int64_t>(cend, nd == pos.end() ? INT64_MAX : *nd);
         const int64_t run = std::min(stop - r, d1 - d);
+        if (run <= 0) return false;
         const PpgInflateJob &J = sh->h_jobs[(size_t)k];
         PpgPackSeg g{};
         g.off = sh->offs.p + E.offst[f][(size_t)k];
@@ -473,6 +480,7 @@ void make_segs(const ppg_pairs *p, int f, int64_t d0, int64_t d1, int32_t grp, s
         pl.push_back(SegPlace{grp});
         d += run;
     }
+    return true;
 }
 
 template <class B>
@@ -555,7 +563,7 @@ int pack_window(ppg_pairs *p, int64_t e, int64_t J, int64_t pairs, Clock::time_p
     for (int f = 0; f < 2; f++) {
         for (int64_t j = e; j < J; j++) {
             const int64_t a = j == e ? e * K + E.cnrec[f] : j * K, z = std::min((j + 1) * K, pairs);
-            make_segs(p, f, a, z, (int32_t)(j - e), seg[f], pl[f]);
+            if (!make_segs(p, f, a, z, (int32_t)(j - e), seg[f], pl[f])) return PPG_DATA_ERROR;
         }
         if (int rc = seg_bounds(E, seg[f], shard_stream(E.sh[f]))) return rc;
     }
@@ -638,7 +646,7 @@ int carry_rest(ppg_pairs *p, int f, int64_t cend, int32_t b) {
     hipStream_t s = shard_stream(E.sh[f]);
     std::vector<PpgPackSeg> seg;
     std::vector<SegPlace> pl;
-    make_segs(p, f, cend, E.bhi[f][(size_t)b], 0, seg, pl);
+    if (!make_segs(p, f, cend, E.bhi[f][(size_t)b], 0, seg, pl)) return PPG_DATA_ERROR;
     if (int rc = seg_bounds(E, seg, s)) return rc;
     int64_t add = 0, nadd = 0;
     for (auto &g : seg) {
@@ -747,6 +755,7 @@ int fused_collected(ppg_pairs *p, int f, int32_t b) {
     }
     E.blo[f].push_back(dedup_of(E.pos[f], r0));
     E.bhi[f].push_back(dedup_of(E.pos[f], r1));
+    E.kvalid[f] = b1;
     if ((size_t)b + 1 == sh->batches.size()) {
         const int rc = shard_finish(sh, E.run_ms[f]);
         sh->last_rc = rc;
@@ -862,15 +871,19 @@ int emit_exchange(ppg_pairs *p, int64_t *j0, int64_t *j1) {
         std::vector<SegPlace> pl;
         std::vector<int32_t> pdst;   // owner of each piece
         int32_t np = 0;
-        for (int32_t r = 0; r < R; r++) {
+        for (int32_t r = 0; r < R && status == PPG_OK; r++) {
             const int64_t a = std::max(h0, own_lo(r)), z = std::min(h1, own_hi(r));
             for (int64_t lo = a; lo < z;) {
                 const int64_t hi = std::min(z, (lo / K + 1) * K);
-                make_segs(p, f, lo - h0, hi - h0, np++, seg, pl);
+                if (!make_segs(p, f, lo - h0, hi - h0, np++, seg, pl)) {
+                    status = PPG_DATA_ERROR;
+                    break;
+                }
                 pdst.push_back(r);
                 lo = hi;
             }
         }
+        if (status != PPG_OK) break;
         status = seg_bounds(E, seg, s);
         if (status != PPG_OK) break;
         piece_len[f].assign((size_t)np, 0);
@@ -1129,6 +1142,7 @@ int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *c
             E.offst[f][(size_t)k] = o;
             o += sh->h_jobs[(size_t)k].raw_shift;
         }
+        E.kvalid[f] = sh->n;
         E.pos[f].resize(p->dp[f].size());
         for (size_t t = 0; t < p->dp[f].size(); t++) E.pos[f][t] = p->dp[f][t] + (int64_t)t;
         // each batch's deduplicated record range
@@ -1195,6 +1209,7 @@ int ppg_pairs_emit_run(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, int64_t pair_
         E.done[f] = false;
         E.run_ms[f] = 0;
         E.batch[f] = -1;
+        E.kvalid[f] = 0;
         E.blo[f].clear();
         E.bhi[f].clear();
         E.pos[f].clear();
