@@ -267,9 +267,12 @@ struct PhaseClock {
         t = now;
         if (n >= (int)sizeof buf) n = (int)sizeof buf - 1;
     }
-    void dump(size_t reqs) {
-        if (on) fprintf(stderr, "PPG_CHUNK launch of %zu: total %.3f ms:%s\n", reqs,
-                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), buf);
+    // (at: the launch's start, ms on the steady clock -- overlapping launches of several slots line up)
+    void dump(size_t reqs, int slot) {
+        if (on)
+            fprintf(stderr, "PPG_CHUNK launch of %zu: total %.3f ms: slot %d at %.3f:%s\n", reqs,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), slot,
+                    std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), buf);
     }
 };
 
@@ -844,7 +847,7 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     if (rec_bytes) HIPCHK(hipMemcpyAsync(sl.res.p + rec_at, sh->recs.p, rec_bytes, hipMemcpyDeviceToHost, sl.s));
     HIPCHK(hipStreamSynchronize(sl.s));
     pc.mark("d2h");
-    pc.dump(go.size());
+    pc.dump(go.size(), (int)(&sl - svc.slot));
     for (size_t i = 0; i < go.size(); i++) {
         ChunkReq *r = go[i];
         const PpgInflateResult &res = sh->h_res[i];
