@@ -54,14 +54,8 @@ template <int RB, int LBT, typename RingT = uint8_t>
 struct __attribute__((aligned(16))) InflateLds {
     // first: the decode's five-word reads address it with ds_read2 offsets (8-bit dword fields)
     uint32_t stream[132];          // compressed words: segment g (32 words) at slot g & 3; [128,132) mirror [0,4)
-    // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1); DecompressAll: 256 more bytes
-    // after the ring hold the identity table (byte b at RING + b), so the pipelined emit loads a
-    // literal lane's byte with the same ds_read_u8 as a match lane's source (PPG_V_IDT)
-#ifdef PPG_V_IDT
-    RingT ring[(1u << RB) + (std::is_same<RingT, uint8_t>::value ? 256 : 0)];
-#else
+    // bytes (DecompressAll) or 16-bit symbols (CreateIndex pass 1)
     RingT ring[1u << RB];
-#endif
     union {                        // the code-length code is dead once the litlen table is built
         uint32_t lit[1 << LBT];
         uint32_t cl[1 << CB];
@@ -578,10 +572,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         }
     } else {
         // history: the last RING bytes of the Point's window -> ring slots of positions [-RING, 0)
-#ifdef PPG_V_IDT
-        // the identity table after the ring (lane l: bytes 4l..4l+3)
-        *(uint32_t *)&S.ring[RING + 4 * lane] = 0x03020100u + 0x04040404u * (uint32_t)lane;
-#endif
         for (uint32_t w0 = 0; w0 < RING / 4; w0 += 64) {
             const uint32_t w = w0 + lane;
             const uint32_t v = *(const uint32_t *)(dict + 32768 - RING + 4 * w);
@@ -1061,21 +1051,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 const uint64_t h2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(inf);
                 hs_look += h2 - h1;
 #endif
-#ifdef PPG_V_EARLYW
-                // the next round's words before the finish when their segments are resident (no DMA to
-                // issue): their LDS latency then runs behind the finish's far-byte merge and ring write
-                {
-                    const uint32_t g = (bp + R.adv) >> 10;
-                    if (g == r.sg || g + 1 == r.sg) {
-                        W = words(bp + R.adv);
-                        finish();
-                    } else {
-                        finish();
-                        st_enter(r, S.stream, g, lane);
-                        W = words(bp + R.adv);
-                    }
-                }
-#else
                 finish();
 #ifdef PPG_STAMPS
                 const uint64_t h3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(
@@ -1088,29 +1063,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 // above, profiles/r04l_ab_pipeline_variants.json)
                 st_enter(r, S.stream, (bp + R.adv) >> 10, lane);
                 W = words(bp + R.adv);
-#endif
 #ifdef PPG_STAMPS
                 const uint64_t h4 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(W.x4);
                 hs_words += h4 - h3;
 #endif
                 const int32_t jj = lane - 1 - (int32_t)(inf >> 17);
-#ifdef PPG_V_IDT
-                if constexpr (IX) {
-                    const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
-                    p_val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
-                } else {
-                    // one load for every lane: a literal's byte from the identity table (few distinct
-                    // addresses: broadcast, not random ring slots), a match's source from the ring; no
-                    // select after it, so the load is waited for only in the next round's finish
-                    const uint32_t ridx = ((inf >> 8) & 511u) == 1u ? RING + ((inf >> 17) & 255u)
-                                                                     : ((rb0 + pos + (uint32_t)jj) & RM);
-                    p_val = S.ring[ridx];
-                }
-#else
                 const uint32_t rv = S.ring[(rb0 + pos + (uint32_t)jj) & RM];
                 if constexpr (IX) p_val = ((inf >> 8) & 511u) != 1u ? rv : (0x8000u | ((inf >> 17) & 255u));
                 else p_val = ((inf >> 8) & 511u) != 1u ? rv : ((inf >> 17) & 255u);
-#endif
                 const bool far = jj < -(int32_t)(RING - 64);
                 // pos >= 32768: every far source is the flushed output; a compiler-tracked load (its
                 // s_waitcnt lands at the first use, in finish)
