@@ -117,6 +117,24 @@ public sealed unsafe class GpuPairedFASTQ : IEnumerable<(FastqRecord R1, FastqRe
         }
     }
 
+    /// <summary>Pair chunks of two shards that have not run (each with ppg_shard_set_keys), the windows
+    /// driving their run (ppg_pairs_emit_run): every output batch decoded once and its halves packed
+    /// while resident -- for shards larger than HBM -- then the check over the keys they wrote.</summary>
+    public static IEnumerable<(long J, FastqRecord[] R1, FastqRecord[] R2)> EmitRun(nint pairs, nint shardR1,
+        nint shardR2, int pairChunk, long windowBytes = 0)
+    {
+        PpGpu.Check(PpGpu.ppg_pairs_emit_run(pairs, shardR1, shardR2, pairChunk, windowBytes));
+        for (;;)
+        {
+            int rc = PpGpu.ppg_pairs_emit_next(pairs, out long j0, out long j1);
+            if (rc == 1) break;
+            PpGpu.Check(rc);
+            for (long j = j0; j < j1; j++) yield return (j, Half(pairs, j, 0), Half(pairs, j, 1));
+        }
+        PpGpu.Check(PpGpu.ppg_pairs_check(pairs, shardR1, shardR2, 0, out var r));
+        if (r.Mismatches != 0) throw new InvalidDataException($"R1/R2 pairing broken at pair {r.FirstBad}");
+    }
+
     // one half: its bytes and descriptors in one copy each, FastqRecords over them
     private static FastqRecord[] Half(nint pairs, long j, int file)
     {
