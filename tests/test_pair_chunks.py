@@ -224,6 +224,51 @@ def test_emit_refuses_bad_use(pair_files, device):
         pr.chunk(j1 + 5, 0)
 
 
+def test_emit_run_edges(pair_files, device):
+    """ppg_pairs_emit_run: shards without keys are refused; one pair chunk larger than all the
+    pairs; a 1-byte window budget (one pair chunk per window); an emission stopped early leaves the
+    shards unrun (the check refuses them) and a new emit_run starts over from their first batch."""
+    gz, chunks, recs, nrec = pair_files
+    ix = [pp.Core.BuildDeflateIndex(g, c) for g, c in zip(gz, chunks)]
+
+    def fresh(keys=True):
+        out = []
+        for g, i in zip(gz, ix):
+            _, i0, _, _ = i.point_fields(0)
+            _, i1, _, _ = i.point_fields(i.Count - 1)
+            s_ = pp.Shard(i, np.frombuffer(g[i0 - 1:i1], np.uint8), 0, i.Count - 1, device=device, out_capacity=2 << 20)
+            if keys:
+                paired.attach_keys(s_, 400_000)
+            out.append(s_)
+        return out
+    pr = paired.Pairs()
+    bare = fresh(keys=False)
+    with pytest.raises(pp.PpgError):
+        next(pr.emit_run(bare[0], bare[1], 1000))
+    sh = fresh()
+    seen = set()
+    wins = list(pr.emit_run(sh[0], sh[1], 10 * nrec))
+    assert wins == [(0, 1)]
+    check_window(pr, 0, 1, 10 * nrec, recs, nrec, seen)
+    seen = set()
+    n = 0
+    for j0, j1 in pr.emit_run(sh[0], sh[1], 5000, window_bytes=1):
+        assert j1 == j0 + 1
+        check_window(pr, j0, j1, 5000, recs, nrec, seen)
+        n += 1
+    assert n == -(-nrec // 5000)
+    it = pr.emit_run(sh[0], sh[1], 3000)
+    next(it)
+    it.close()
+    with pytest.raises(pp.PpgError):   # stopped early: the shards have not run
+        pr.check(sh[0], sh[1])
+    seen = set()
+    for j0, j1 in pr.emit_run(sh[0], sh[1], 3000):
+        check_window(pr, j0, j1, 3000, recs, nrec, seen)
+    assert seen == set(range(-(-nrec // 3000)))
+    assert pr.check(sh[0], sh[1])["mismatches"] == 0
+
+
 def _emit_rank(rank, world, name, gz, chunks, K, q):
     try:
         import parallelparsing_amd as pp2
