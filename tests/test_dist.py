@@ -213,7 +213,10 @@ def _a2a_rank(rank, world, name, counts, q):
 def test_host_alltoallv_in_rounds(world):
     """ppg_comm_alltoallv over the host transport (the paired-read key exchange's collective,
     ppg_pairs_check, rehearsed on a one-GPU box): uneven counts, zero counts and counts larger than
-    one round of the shared slots (8 MiB per rank) arrive complete and in source order.  No GPU."""
+    one round of the shared slots (8 MiB per rank) arrive complete and in source order.  No GPU.
+    The RCCL form of the same exchange (grouped ncclSend / ncclRecv over xGMI) has not run with more
+    than one GPU: only its error paths are covered, with fake entry points
+    (tests/native/host_check.cpp, run under ASan / TSan by tests/test_sanitizers.py)."""
     import uuid
     import torch.multiprocessing as mp
     rng = np.random.default_rng(world)
