@@ -19,6 +19,7 @@ import os
 import numpy as np
 
 from ._lib import lib, check, PpgError, PPG_NO_DEVICE, PPG_STREAM_END, PpgBatch, synth  # noqa: F401
+from . import _lib
 
 WINSIZE = 32768
 CHUNK = 16384
@@ -364,13 +365,21 @@ class Core:
         o1, _, _, _ = index.point_fields(k + 1)
         need = max(0, o1 - o0)
         if buf is None:
-            buf = np.zeros(need, np.uint8)
+            buf = np.empty(need, np.uint8)   # every produced byte is written
         produced = C.c_int64()
         nrec = C.c_int64()
-        recs = np.zeros((max(1, need // 4 + 1), 4), np.uint32) if with_records else None
-        check(lib.ppg_decompress_chunk(dev.handle, index.handle, int(k), _ptr(src), src.size, _ptr(buf), buf.size,
-                                       C.byref(produced), _ptr(recs), recs.shape[0] if with_records else 0,
-                                       C.byref(nrec)), "Core.ExtractDeflateIndex")
+        # descriptor rows for >= 64-B records (a FASTQ record is hundreds); a chunk of smaller ones
+        # reports its record count with PPG_BUF_ERROR and is decoded again into an exact table
+        # (r05: rows for 4-B records made every call zero 4x its output bytes in the allocator)
+        recs = np.empty((_rec_rows(need), 4), np.uint32) if with_records else None
+        rc = lib.ppg_decompress_chunk(dev.handle, index.handle, int(k), _ptr(src), src.size, _ptr(buf), buf.size,
+                                      C.byref(produced), _ptr(recs), recs.shape[0] if with_records else 0,
+                                      C.byref(nrec))
+        if with_records and rc == _lib.PPG_BUF_ERROR and nrec.value > recs.shape[0]:
+            recs = np.empty((nrec.value, 4), np.uint32)
+            rc = lib.ppg_decompress_chunk(dev.handle, index.handle, int(k), _ptr(src), src.size, _ptr(buf), buf.size,
+                                          C.byref(produced), _ptr(recs), recs.shape[0], C.byref(nrec))
+        check(rc, "Core.ExtractDeflateIndex")
         if with_records:
             return produced.value, buf, recs[:nrec.value]
         return produced.value, buf
@@ -387,11 +396,16 @@ class Core:
         need = max(0, o1 - o0)
         if buf is None:
             buf = np.empty(need, np.uint8)
-        recs = np.empty((max(1, need // 4 + 1), 4), np.uint32)
+        recs = np.empty((_rec_rows(need), 4), np.uint32)   # (too few: result() decodes it again)
         t = C.c_void_p()
         check(lib.ppg_decompress_chunk_submit(dev.handle, index.handle, int(k), _ptr(src), src.size, _ptr(buf), buf.size,
                                               _ptr(recs), recs.shape[0], C.byref(t)), "ppg_decompress_chunk_submit")
-        return ChunkFuture(dev, t, (src, buf, recs, index))
+        return ChunkFuture(dev, t, (src, buf, recs, index, k))
+
+
+def _rec_rows(nbytes):
+    """Descriptor rows to offer for a chunk of nbytes of text: enough for records of >= 64 bytes."""
+    return int(nbytes) // 64 + 256
 
 
 class ChunkFuture:
@@ -407,8 +421,11 @@ class ChunkFuture:
             if t is None:
                 raise RuntimeError("ChunkFuture waited twice")
             rc = lib.ppg_decompress_chunk_wait(self._dev.handle, t, C.byref(produced), C.byref(nrec))
-            _, buf, recs, _ = self._keep
+            src, buf, recs, index, k = self._keep
             self._keep = None
+            if rc == _lib.PPG_BUF_ERROR and nrec.value > recs.shape[0]:   # records under 64 B: once more, exactly
+                self._res = Core.ExtractDeflateIndex(src, index, k, buf=buf, device=self._dev, with_records=True)
+                return self._res
             check(rc, "Core.ExtractDeflateIndexAsync")
             self._res = (produced.value, buf, recs[:nrec.value])
         return self._res

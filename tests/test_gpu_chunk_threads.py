@@ -155,6 +155,37 @@ def test_lone_chunks_found_side_points_vs_oracle():
     assert split == n and pts >= 2 * n, (split, pts)
 
 
+def test_tiny_records_get_an_exact_table():
+    """Records far under the wrappers' 64-B sizing ("@\nA\n+\n!\n": 8 bytes): the library reports
+    the chunk's record count with PPG_BUF_ERROR and the wrapper decodes it again into an exact
+    table -- synchronously and through the asynchronous entry point -- equal to the oracle's."""
+    import zlib
+    recs = [b"@%d\n%s\n+\n%s\n" % (i % 10, b"ACGT"[i % 4:i % 4 + 1], b"!?*"[i % 3:i % 3 + 1])
+            for i in range(60_000)]
+    co = zlib.compressobj(6, zlib.DEFLATED, 31)
+    parts = []
+    for g in range(0, len(recs), 5_000):   # a block end every 5,000 records: Points can fall there
+        parts.append(co.compress(b"".join(recs[g:g + 5_000])))
+        parts.append(co.flush(zlib.Z_FULL_FLUSH))
+    parts.append(co.flush())
+    gz = b"".join(parts)
+    oi = O.build_index(gz, 20_000)
+    ix = pp.Core.BuildDeflateIndex(gz, 20_000)
+    dev = pp.Device(0)
+    n = ix.Count - 1
+    assert n >= 2
+    futs = [pp.Core.ExtractDeflateIndexAsync(slice_of(gz, ix, k), ix, k, device=dev) for k in range(n)]
+    for k in range(n):
+        b = O.extract(gz, oi, k)
+        exp = O.parse(oi.point(k)[4], b)
+        if b:
+            assert len(exp) > len(b) // 64 + 256   # more records than the first table holds
+        got, buf, rec = pp.Core.ExtractDeflateIndex(slice_of(gz, ix, k), ix, k, device=dev, with_records=True)
+        assert got == len(b) and sha(buf[:got]) == sha(b) and np.array_equal(rec, exp), k
+        got, buf, rec = futs[k].result()
+        assert got == len(b) and sha(buf[:got]) == sha(b) and np.array_equal(rec, exp), k
+
+
 def test_threads_side_points_split_chunks(file200k):
     """An index with side points (GPU CreateIndex, side_bytes): each chunk is decoded as one wave
     per piece inside the combined launch -- results identical to the oracle's."""
