@@ -49,7 +49,7 @@ class Index:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and lib is not None:   # (lib is None at interpreter exit)
             lib.ppg_index_free(h)
             self._h = None
 
@@ -172,7 +172,7 @@ class Device:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and lib is not None:   # (lib is None at interpreter exit)
             lib.ppg_close(h)
             self._h = None
 
@@ -464,7 +464,7 @@ class Shard:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and lib is not None:   # (lib is None at interpreter exit)
             lib.ppg_shard_free(h)
             self._h = None
 

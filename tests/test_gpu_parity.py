@@ -145,6 +145,46 @@ def test_larger_file_vs_oracle_and_trailer(device):
     assert tot == sh.total_records == nrec   # zlib -6 never places a Point at a record start here
 
 
+@pytest.mark.parametrize("level,strategy,wbits,mem", [(1, zlib.Z_DEFAULT_STRATEGY, 15, 8),
+                                                       (9, zlib.Z_DEFAULT_STRATEGY, 15, 9),
+                                                       (4, zlib.Z_FILTERED, 15, 8),
+                                                       (6, zlib.Z_RLE, 15, 8),
+                                                       (6, zlib.Z_DEFAULT_STRATEGY, 9, 1),
+                                                       (3, zlib.Z_FIXED, 12, 4)])
+def test_encoder_variants_vs_oracle(level, strategy, wbits, mem, device):
+    """One member from each of several zlib encoder settings (level, strategy, window bits --
+    shorter windows mean shorter match distances --, memLevel: block sizes), 20k records, chunk
+    1,000: DecompressAll (every chunk) and the lone-chunk Decompress path (its inner block starts
+    found on the GPU, pieces written out from their symbols) against the oracle, bytes and records,
+    plus the CRC-32 of the whole output against the gzip trailer."""
+    import ctypes as C
+    S = pp.synth()
+    nrec = 20_000
+    sz = S.ppg_synth_fastq_size(0, nrec, 150)
+    txt = np.zeros(sz, np.uint8)
+    S.ppg_synth_fastq(level * 7 + wbits, 0, nrec, 150, C.c_void_p(txt.ctypes.data), sz, 8)
+    co = zlib.compressobj(level, zlib.DEFLATED, 16 + wbits, mem, strategy)
+    gz = co.compress(txt.tobytes()) + co.flush()
+    ix = pp.Core.BuildDeflateIndex(gz, 1000)
+    oi = O.build_index(gz, 1000)
+    n = ix.Count - 1
+    assert n == oi.count - 1 and n >= 5
+    sh = pp.Shard(ix, comp_range(gz, ix, 0, n), 0, n, device=device).run()
+    crc = 0
+    for k in range(n):
+        exp = O.extract(gz, oi, k)
+        rexp = O.parse(oi.point(k)[4], exp)
+        b = sh.chunk_bytes(k)
+        assert b.tobytes() == exp, k
+        assert np.array_equal(sh.chunk_records(k), rexp), k
+        crc = zlib.crc32(b.tobytes(), crc)
+        if k % 4 == 1:
+            got, buf, rec = pp.Core.ExtractDeflateIndex(comp_range(gz, ix, k, 1), ix, k, device=device,
+                                                        with_records=True)
+            assert buf[:got].tobytes() == exp and np.array_equal(rec, rexp), k
+    assert crc == int.from_bytes(gz[-8:-4], "little")
+
+
 @pytest.mark.parametrize("name,piece", [("l6_c20", 1), ("memlevel1_c10", 20000), ("stored_c50", 1),
                                         ("pigz_c100", 1 << 30), ("huffonly_c20", 50000)])
 def test_file_ingest_matches_golden(name, piece, tmp_path, device):
