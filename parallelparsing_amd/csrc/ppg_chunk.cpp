@@ -5,18 +5,22 @@
 // The reference calls this once per chunk from a ThreadPool task per chunk (BatchedFASTQ.cs:62-77),
 // each with its own ZStream.  On the GPU one chunk alone is one wave of the 8,192 the chip holds,
 // so concurrent calls are *combined*: a call queues its request, and whichever waiting caller finds
-// one of the ctx's two launch slots free takes every queued request into one launch (flat
-// combining -- no service thread).  While a launch runs, new calls queue up for the other slot, so
-// T callers keep up to T chunks in flight in at most two launches.
+// one of the ctx's four launch slots free takes the queued requests (up to 256) into one launch
+// (flat combining).  A second launch starts beside a running one only once 16 requests queue, so
+// the queue that builds during a launch goes into the next one.  Asynchronous requests
+// (ppg_decompress_chunk_submit) are launched the same way by a launcher thread of the ctx, which
+// also copies their results out.
 //
 // A slot owns everything a launch touches -- its stream, a one-batch ppg_shard, the gathered
-// compressed slices (pinned + device), the pinned copy of the outputs and descriptors -- and its
-// buffers only grow (geometrically), so a warm ctx makes no hipMalloc/hipFree per call: hipFree
-// waits for the whole device.  Each caller copies its own chunk out of the slot's pinned results
-// in parallel with the others; the slot is reused only after every such copy is done.
+// compressed slices (pinned + device), the pinned copy of the outputs and descriptors, the block
+// search's scratch -- and its buffers only grow (geometrically), so a warm ctx makes no
+// hipMalloc/hipFree per call: hipFree waits for the whole device.  Each synchronous caller copies
+// its own chunk out of the slot's pinned results in parallel with the others; the slot is reused
+// only after every such copy is done.
 //
 // Chunks whose index carries side points (ppg_index_build_gpu_side) are decoded as one wave per
-// piece between their inner block starts (ppg_shard_set_split), exactly as DecompressAll does.
+// piece between their inner block starts (ppg_shard_set_split), exactly as DecompressAll does; the
+// others get theirs found on the GPU (find_side_points, find_mat below).
 #include "ppg_host.h"
 #include <atomic>
 #include <chrono>
@@ -153,9 +157,7 @@ int find_sub(int ranges) { return std::max(1, std::min(32, 16384 / std::max(1, r
 // device scratch of find_side_points (grow only)
 struct FindScratch {
     DevBuf<uint16_t> sym;                  // materialise path: every piece's pass-1 symbols, whole
-    DevBuf<PpgMatInfo> mi;
-    DevBuf<PpgInflateJob> lj;              // its launch order
-    DevBuf<uint32_t> linv;
+    DevBuf<PpgMatInfo> mi;                 // ... and each materialised piece's info
     DevBuf<uint64_t> lo, hi, cand;
     DevBuf<PpgInflateJob> jobs;
     DevBuf<PpgInflateResult> res;
