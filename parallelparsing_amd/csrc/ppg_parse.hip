@@ -304,17 +304,30 @@ extern "C" __global__ __launch_bounds__(256) void ppg_parse_place(
     const uint64_t limit = 4 * f.records;
     uint32_t *dst = recs + 4 * base[k];
     const uint32_t onl = oref[k].nl & PPG_OFF_COUNT;
-    if (onl && threadIdx.x == 0) {
+    if (onl) {
+        // the offset's newlines by the whole block, 256 bytes a step (ballot + wave counts): one
+        // thread's byte loop over the offset (~400 B) held every block open while the other 255
+        // copied (r05: 5.7 ms of the 50 GB step)
+        __shared__ uint32_t wcnt[4];
         const uint8_t *off = offs + oref[k].start;
-        uint64_t m = 0;
-        for (uint32_t i = 0, n = oref[k].len; i < n && m < limit; i++)
-            if (off[i] == '\n') dst[m++] = i;
+        const uint32_t n = oref[k].len, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+        uint64_t m = 0;   // the offset's newlines before this step
+        for (uint32_t g = 0; g < n; g += 256) {
+            const uint32_t i = g + threadIdx.x;
+            const bool nl = i < n && off[i] == '\n';
+            const uint64_t b = __ballot(nl);
+            if (lane == 0) wcnt[wv] = (uint32_t)__popcll(b);
+            __syncthreads();
+            uint64_t idx = m + (uint64_t)__popcll(b & ((1ull << lane) - 1ull));
+            for (uint32_t q = 0; q < wv; q++) idx += wcnt[q];
+            if (nl && idx < limit) dst[idx] = i;
+            m += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            __syncthreads();
+        }
     }
     if (limit <= onl) return;
     const uint64_t cnt = min(limit - onl, (uint64_t)ires[k].newlines);
     const uint32_t *src = nls + jobs[k].nl_off;
-    // (r05: eight loads in flight per thread measured the same 5.7 ms per 50 GB step: ~17 GB moved
-    // at ~3 TB/s, census positions read + descriptors written)
     for (uint64_t i = threadIdx.x; i < cnt; i += 256) dst[onl + i] = src[i];
 }
 
