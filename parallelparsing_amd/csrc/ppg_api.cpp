@@ -1071,6 +1071,7 @@ struct IngestState {
     DevBuf<uint8_t> db[kPieces];  // device copies of pieces
     hipStream_t cs = nullptr;     // copy stream
     hipStream_t ks[kPieces] = {};   // decode streams, one per piece slot
+    hipEvent_t piece_ev[kPieces] = {};   // the piece's bytes are on the device (recorded on cs)
     ppg_shard *sh[kPieces] = {};
 };
 
@@ -1078,8 +1079,10 @@ static void ingest_free(IngestState *st) {
     if (!st) return;
     for (int i = 0; i < kSlots; i++)
         if (st->slot_ev[i]) (void)hipEventDestroy(st->slot_ev[i]);
-    for (int i = 0; i < kPieces; i++)
+    for (int i = 0; i < kPieces; i++) {
         if (st->sh[i]) ppg_shard_free(st->sh[i]);
+        if (st->piece_ev[i]) (void)hipEventDestroy(st->piece_ev[i]);
+    }
     if (st->cs) (void)hipStreamDestroy(st->cs);
     for (auto &k : st->ks) if (k) (void)hipStreamDestroy(k);
     delete st;
@@ -1153,6 +1156,7 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             st->sh[i] = new ppg_shard;
             st->sh[i]->ctx = ctx;
             HIPCHK(hipStreamCreateWithFlags(&st->ks[i], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&st->piece_ev[i], hipEventDisableTiming));
             st->sh[i]->stream = st->ks[i];
         }
     }
@@ -1163,9 +1167,11 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
     }
     if (verbose) fprintf(stderr, "[ingest] %zu pieces, max %.1f MB, setup %.1f ms\n", pieces.size(), maxlen / 1e6, now_ms());
 
-    // Producer thread: piece k -> device buffer k&1 (pread into pinned slots, H2D on the copy
-    // stream, slot by slot), then its jobs/windows/offsets (shard_prepare, which syncs the copy
-    // stream).  Consumer (this thread): decodes piece k once ready.  At most two pieces in flight.
+    // Producer thread: piece k -> device buffer k % kPieces (pread into pinned slots, H2D on the
+    // copy stream, slot by slot), an event when its bytes are there.  Consumer (this thread): piece
+    // k's jobs / windows / offsets (shard_prepare, on the piece's decode stream, which waits for that
+    // event on the device), then its launch -- so a piece's prepare (~14 ms at 8 GiB: 9k windows
+    // staged and copied) overlaps the next piece's read instead of delaying it (r05).
     const size_t np = pieces.size();
     std::mutex mu;
     std::condition_variable cv;
@@ -1194,17 +1200,12 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
                     hipEventRecord(S.slot_ev[slot], S.cs) != hipSuccess)
                     rcp = PPG_DEVICE_ERROR;
             }
-            const double t2 = now_ms();
-            if (rcp == PPG_OK && hipMemsetAsync(dst + len, 0, 64, S.cs) != hipSuccess) rcp = PPG_DEVICE_ERROR;
-            if (rcp == PPG_OK)
-                rcp = shard_prepare(S.sh[k % kPieces], ix, first + pieces[k].first, pieces[k].second - pieces[k].first, dst,
-                                    len, 0, S.cs);
-            if (rcp == PPG_OK && split)
-                rcp = shard_split_from_index(S.sh[k % kPieces], ix, first + pieces[k].first,
-                                             pieces[k].second - pieces[k].first);
+            if (rcp == PPG_OK && (hipMemsetAsync(dst + len, 0, 64, S.cs) != hipSuccess ||
+                                  hipEventRecord(S.piece_ev[k % kPieces], S.cs) != hipSuccess))
+                rcp = PPG_DEVICE_ERROR;
             if (verbose)
-                fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms, prepare %.1f ms\n", k,
-                        len / 1e6, t1, t2 - t1, now_ms() - t2);
+                fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms\n", k, len / 1e6, t1,
+                        now_ms() - t1);
             std::lock_guard<std::mutex> lk(mu);
             if (rcp != PPG_OK) prod_rc = rcp;
             else ready = k + 1;
@@ -1250,9 +1251,18 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             if (ready <= k) { rc = prod_rc; break; }
         }
         ppg_shard *sh = S.sh[k % kPieces];
+        const double tp = now_ms();
+        int64_t off, len;
+        range(k, off, len);
+        if (hipStreamWaitEvent(S.ks[k % kPieces], S.piece_ev[k % kPieces], 0) != hipSuccess) { rc = PPG_DEVICE_ERROR; break; }
+        rc = shard_prepare(sh, ix, first + pieces[k].first, pieces[k].second - pieces[k].first, S.db[k % kPieces].p, len,
+                           0, S.ks[k % kPieces]);
+        if (rc == PPG_OK && split)
+            rc = shard_split_from_index(sh, ix, first + pieces[k].first, pieces[k].second - pieces[k].first);
+        if (rc != PPG_OK) break;
         shard_reset(sh);
         rc = sh->batches.size() == 1 ? batch_launch(sh, 0, sh->n) : PPG_ARG_ERROR;
-        if (verbose) fprintf(stderr, "[ingest] piece %zu: launched at %.1f ms\n", k, now_ms());
+        if (verbose) fprintf(stderr, "[ingest] piece %zu: prepared in %.1f ms, launched at %.1f ms\n", k, now_ms() - tp, now_ms());
         if (rc != PPG_OK) break;
         if (k > 0 && (rc = collect(k - 1)) != PPG_OK) break;
     }
