@@ -150,7 +150,7 @@ int result_spans(const ChunkReq &req, uint8_t *out, int64_t out_cap, uint32_t *r
 }
 
 // waves per candidate range of the block search: enough for ~16,384 waves in all, two generations of
-// the GPU's wave slots (a lone chunk's 16 ranges are searched by 32 waves each; r05: at 4,096 waves a
+// the GPU's wave slots (a lone chunk's 48 ranges are searched by 32 waves each; r05: at 4,096 waves a
 // launch of 256 chunks searched its 3,840 ranges with one wave each, 7.0 ms)
 int find_sub(int ranges) { return std::max(1, std::min(32, 16384 / std::max(1, ranges))); }
 
@@ -469,6 +469,14 @@ int find_side_points(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const
 // + resolve + materialise, instead of that plus a second decode of the same block.
 constexpr int kMatMaxChunks = (int)kMaxBatch;
 constexpr uint64_t kMatRatio = 10;        // symbol capacity per compressed byte of a piece (FASTQ: ~4)
+// candidate ranges per chunk and their least compressed size: a zlib -6 FASTQ block is ~16 K symbols,
+// ~20 KB of gzip, so ranges of ~1/16 chunk (60 KB) held 2-3 block starts of which the finder keeps
+// the first, and the slowest piece was several blocks long.  r05 (tools/chunk_latency.py, one box):
+// 16 ranges / 48 KiB: T = 1 5.68 ms (pass 1 3.8); 24 / 32: 4.72; 32 / 24: 3.94 (2.36); 48 / 16:
+// 2.90 (1.60); 64 / 12: 2.85 (1.61) -- pieces of one block each from 48 on; a 256-chunk launch
+// ~45 ms at every setting (the search grows as pass 1 shrinks)
+constexpr uint64_t kMatRanges = 48;
+constexpr uint64_t kMatMinRange = 16 * 1024;
 
 struct MatPiece {
     uint64_t start, stop;       // bits: piece start, the next piece's start (the chunk's end for the last)
@@ -488,7 +496,7 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     std::vector<size_t> cfirst(ch.size() + 1, 0);
     for (size_t c = 0; c < ch.size(); c++) {
         const uint64_t span = ch[c].bit1 - ch[c].bit0;
-        const uint64_t pb = std::max<uint64_t>(8ull * 48 * 1024, span / 16);
+        const uint64_t pb = std::max<uint64_t>(8ull * kMatMinRange, span / kMatRanges);
         for (uint64_t a = ch[c].bit0 + pb; a + 8ull * 1024 < ch[c].bit1; a += pb) {
             lo.push_back(a);
             hi.push_back(std::min(a + pb, ch[c].bit1));
