@@ -526,7 +526,9 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
             if (cand[k] != ~0ull && cand[k] > st.back() && cand[k] < ch[c].bit_end) st.push_back(cand[k]);
         st.push_back(ch[c].bit_end);
         for (size_t j = 0; j + 1 < st.size(); j++) {
-            const uint64_t cap = std::max<uint64_t>(64 * 1024, kMatRatio * ((st[j + 1] - st[j]) / 8 + 64));
+            // (at least 256 Ki symbols: a piece whose next candidate is false decodes on to the next
+            // real block end, a whole block past a stop that may be only a few KB away)
+            const uint64_t cap = std::max<uint64_t>(256 * 1024, kMatRatio * ((st[j + 1] - st[j]) / 8 + 64));
             pc.push_back(MatPiece{st[j], st[j + 1], syms, cap});
             syms += cap + 2048;   // flushes may run up to a unit past the capacity check
         }
@@ -572,32 +574,49 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     HIPCHK(hipMemcpyAsync(blk.data(), F.blk.p, sizeof(PpgBlockEnd) * nblk, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     clk.mark("f.pass1");
-    // a chunk is covered when its pieces chain from its Point to its end: every piece ends exactly
-    // where the next starts (its last block end), the last exactly at the chunk's end (or with the
-    // final block, for the file's last chunk), and their outputs add up to the chunk's
+    // a chunk is covered when its pieces chain from its Point to its end: each piece's last block
+    // end is where the chain's next piece starts -- normally the next candidate; after a false
+    // candidate (its piece fails, or the piece before it decodes on to the next real block end) the
+    // first later piece that starts there, the false ones skipped (r05: ~0.6% of chunks at 48
+    // ranges fell back to a one-wave decode of ~45 ms) --, the chain's last piece ends exactly at
+    // the chunk's end (or with the final block, for the file's last chunk), and their outputs add up
     std::vector<size_t> wbase(ch.size(), 0);
+    std::vector<std::vector<uint32_t>> chain(ch.size());
     std::vector<uint64_t> E(np, 0);
     size_t nw = 0;
     for (size_t c = 0; c < ch.size(); c++) {
-        bool ok = pfirst[c + 1] > pfirst[c];
         uint64_t tot = 0;
-        for (size_t q = pfirst[c]; ok && q < pfirst[c + 1]; q++) {
+        int why = 0;   // (PPG_CHUNK_VERBOSE: why a chunk is not covered)
+        bool done = false;
+        size_t q = pfirst[c];
+        while (q < pfirst[c + 1]) {
             const PpgInflateResult &r = res[q];
             const uint32_t nb = std::min(r.nblocks, jobs[q].blk_cap);
-            if (r.status != 0 || nb == 0 || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN))) { ok = false; break; }
+            if (r.status != 0 || nb == 0 || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN))) {
+                why = r.status != 0 ? 1 : nb == 0 ? 2 : (r.flags & PPG_FLAG_BLK_FULL) ? 3 : 4;
+                break;
+            }
             const PpgBlockEnd &e = blk[jobs[q].blk_off + nb - 1];
+            if (e.out_end != r.produced) { why = 5; break; }
             E[q] = e.end_bit;
-            if (e.out_end != r.produced) { ok = false; break; }
-            const bool lastp = q + 1 == pfirst[c + 1];
-            if (!lastp && (r.last || e.end_bit != pc[q].stop)) { ok = false; break; }
-            if (lastp && !(e.end_bit == ch[c].bit_end || (r.last && ch[c].bit_end == ch[c].bit1))) { ok = false; break; }
+            chain[c].push_back((uint32_t)q);
             tot += r.produced;
+            if (e.end_bit == ch[c].bit_end || (r.last && ch[c].bit_end == ch[c].bit1)) { done = true; break; }
+            if (r.last) { why = 6; break; }
+            size_t nx = q + 1;   // the piece that starts at this end
+            while (nx < pfirst[c + 1] && pc[nx].start < e.end_bit) nx++;
+            if (nx >= pfirst[c + 1] || pc[nx].start != e.end_bit) { why = 7; break; }
+            q = nx;
         }
-        ok = ok && (int64_t)tot == ch[c].len;
+        if (done && (int64_t)tot != ch[c].len) why = 9;
+        const bool ok = done && (int64_t)tot == ch[c].len;
+        if (!ok && clk.on)
+            fprintf(stderr, "PPG_CHUNK not covered: chunk %zu reason %d after %zu chained of %zu pieces\n", c, why,
+                    chain[c].size(), pfirst[c + 1] - pfirst[c]);
         covered[c] = ok;
         if (ok) {
             wbase[c] = nw;
-            nw += pfirst[c + 1] - pfirst[c];
+            nw += chain[c].size();
         }
     }
     if (!nw) return PPG_OK;
@@ -618,8 +637,8 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     std::vector<uint4> cs;
     for (size_t c = 0; c < ch.size(); c++) {
         if (!covered[c]) continue;
-        for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) sl_all[wbase[c] + (q - pfirst[c])] = (uint32_t)q;
-        cs.push_back(uint4{(uint32_t)wbase[c], (uint32_t)(pfirst[c + 1] - pfirst[c]), ch[c].win, 0});
+        std::copy(chain[c].begin(), chain[c].end(), sl_all.begin() + (ptrdiff_t)wbase[c]);
+        cs.push_back(uint4{(uint32_t)wbase[c], (uint32_t)chain[c].size(), ch[c].win, 0});
     }
     HIPCHK(grow_buf(F.chains, cs.size()));
     HIPCHK(hipMemcpyAsync(F.slots.p, sl_all.data(), 4 * nw, hipMemcpyHostToDevice, s));
@@ -629,8 +648,8 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     for (size_t c = 0; c < ch.size(); c++) {
         if (!covered[c]) continue;
         uint64_t outc = 0, last_end = 0;
-        for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) {
-            const size_t j = q - pfirst[c];
+        for (size_t j = 0; j < chain[c].size(); j++) {
+            const size_t q = chain[c][j];
             last_end = E[q];
             if (res[q].produced == 0) continue;   // an empty piece (a flush block) adds nothing
             if (!pmi[c].empty()) {
@@ -697,7 +716,7 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
             const auto &O = r->ix->side_out;
             nsub += (size_t)std::max<std::ptrdiff_t>(0, std::lower_bound(O.begin(), O.end(), to.output) -
                                                             std::upper_bound(O.begin(), O.end(), from.output));
-            if (O.empty() && n <= (size_t)kFindMaxChunks) nsub += 16;   // find_side_points' at most
+            if (O.empty() && n <= (size_t)kFindMaxChunks) nsub += kMatRanges;   // the block search's at most
         }
         ppg_shard *sh = sl.sh;
         HIPCHK(grow_buf(sh->jobs, n));
@@ -787,8 +806,8 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
                 lj[q] = sh->h_sjobs[order[q]];
                 inv[order[q]] = (uint32_t)q;
             }
-            HIPCHK(sh->ljobs.alloc(ns));
-            HIPCHK(sh->linv.alloc(ns));
+            HIPCHK(grow_buf(sh->ljobs, ns));   // (grow-only with headroom: a hipFree waits for the
+            HIPCHK(grow_buf(sh->linv, ns));    // whole device, every other slot's launch included)
             HIPCHK(grow_buf(sl.fs.mi, lmi.size()));
             HIPCHK(hipMemcpyAsync(sh->ljobs.p, lj.data(), sizeof(PpgInflateJob) * ns, hipMemcpyHostToDevice, sl.s));
             HIPCHK(hipMemcpyAsync(sh->linv.p, inv.data(), 4 * ns, hipMemcpyHostToDevice, sl.s));
