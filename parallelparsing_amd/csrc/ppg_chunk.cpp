@@ -526,9 +526,10 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
             if (cand[k] != ~0ull && cand[k] > st.back() && cand[k] < ch[c].bit_end) st.push_back(cand[k]);
         st.push_back(ch[c].bit_end);
         for (size_t j = 0; j + 1 < st.size(); j++) {
-            // (at least 256 Ki symbols: a piece whose next candidate is false decodes on to the next
-            // real block end, a whole block past a stop that may be only a few KB away)
-            const uint64_t cap = std::max<uint64_t>(256 * 1024, kMatRatio * ((st[j + 1] - st[j]) / 8 + 64));
+            // (at least 192 Ki symbols, ~1.5 zlib -6 FASTQ blocks: a piece whose next candidate is false
+            // decodes on to the next real block end, a whole block past a stop that may be only a few
+            // KB away; a piece of a typical ~20 KB range gets its 10x anyway, so the floor costs little)
+            const uint64_t cap = std::max<uint64_t>(192 * 1024, kMatRatio * ((st[j + 1] - st[j]) / 8 + 64));
             pc.push_back(MatPiece{st[j], st[j + 1], syms, cap});
             syms += cap + 2048;   // flushes may run up to a unit past the capacity check
         }
