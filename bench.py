@@ -18,6 +18,7 @@ consumer enumerating records would.
   N > 1 defaults to strong scaling: one ~50 GB member split over the N GPUs (configs[3]).
 """
 import argparse
+import gc
 import json
 import os
 import socket
@@ -413,9 +414,7 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
         finally:
             os.environ.pop("PPG_CHUNK_NO_FIND", None)
 
-    def async_leg(ix, depth):
-        """One caller thread queues `depth` chunks (ppg_decompress_chunk_submit) and then takes the
-        results in order (ppg_decompress_chunk_wait)."""
+    def async_once(ix, depth):
         n = min(nmax, depth)
         before = dev.decompress_chunk_stats()
         t = time.perf_counter()
@@ -427,9 +426,17 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
         return {"chunks": n, "records_per_s": float(got.sum()) / sec, "chunks_per_s": n / sec, "seconds": sec,
                 "launches": after["launches"] - before["launches"]}
 
-    # warm: the launcher thread, and every launch slot's buffers grown to a full launch (256 chunks
-    # each; r05: warming one slot left depth 1024 at 16.5 M records/s against 30.4 for depth 256)
-    async_leg(plain, nmax)
+    def async_leg(ix, depth):
+        """One caller thread queues `depth` chunks (ppg_decompress_chunk_submit) and then takes the
+        results in order (ppg_decompress_chunk_wait): one untimed run, then the median of 3 (a launch
+        slot first used grows its block-search scratch by GBs, hipFree + hipMalloc; r05: a slot first
+        used inside the timed depth-1024 run took 3.85 s there)."""
+        async_once(ix, depth)
+        runs = sorted((async_once(ix, depth) for _ in range(3)), key=lambda r: r["records_per_s"])
+        return runs[1]
+
+    # warm: the launcher thread, and the launch slots' buffers grown to full launches (256 chunks each)
+    async_once(plain, nmax)
     leg(plain, 8)
     out = {f"T{T}": leg(plain, T) for T in threads_list}
     out["async"] = {f"depth{d}": async_leg(plain, d) for d in (256, 1024)}
@@ -1141,20 +1148,28 @@ def main():
                                                                for x, y in setup_ranks]},
     }
     args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines and args.share == 1
-    if rank == 0 and world == 1 and (args.ingest or args.create_index):
+    chunk_legs = world == 1 and args.workload == "50gb" and not args.no_chunk_api and args.share == 1
+    if rank == 0 and world == 1 and (args.ingest or args.create_index or chunk_legs):
+        # the measured shard (~270 GB of HBM at configs[2]) is done with: the legs below get the device
         del shard, comp
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and args.create_index:
         line["create_index"] = create_index_run(tf, args, dev)
     if rank == 0 and world == 1 and args.ingest:
+        # a ctx of its own: its ingest buffers (three 8 GiB pieces and their shards' outputs) are
+        # freed with it, before the per-chunk legs
+        ictx = pp.Device(ctx.device)
         try:
-            line["ingest"], enum = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads,
+            line["ingest"], enum = ingest_run(tf, tf.index(0, tf.npoints), ictx, args.host_threads,
                                               args.ingest_piece_gib, 0 if args.no_enumerate else args.enum_batch_gib)
             if enum is not None:
                 line["enumerate"] = enum
         except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
             line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
-    if rank == 0 and world == 1 and args.workload == "50gb" and not args.no_chunk_api and args.share == 1:
+        finally:
+            del ictx
+            gc.collect()
+    if rank == 0 and chunk_legs:
         try:
             line["decompress_chunk"] = decompress_chunk_run(tf, ctx, r["records"])
         except (AssertionError, RuntimeError, pp.PpgError) as e:

@@ -149,6 +149,23 @@ int result_spans(const ChunkReq &req, uint8_t *out, int64_t out_cap, uint32_t *r
     return PPG_OK;
 }
 
+// grow a big scratch buffer of the block search; out of device memory (e.g. beside a resident
+// DecompressAll shard) is not a failure of the requests: the caller decodes them whole instead
+#define GROW_OR_SKIP(b, n)                                                                      \
+    do {                                                                                        \
+        const hipError_t grow_e = grow_buf(b, n);                                               \
+        if (grow_e == hipErrorOutOfMemory) {                                                    \
+            (void)hipGetLastError();                                                            \
+            fprintf(stderr, "ppgpu: block search scratch %s of %zu elements: out of device memory, " \
+                    "the launch's chunks decoded whole\n", #b, (size_t)(n));                   \
+            return PPG_MEM_ERROR;                                                               \
+        }                                                                                       \
+        if (grow_e != hipSuccess) {                                                             \
+            fprintf(stderr, "ppgpu: grow %s failed: %s\n", #b, hipGetErrorString(grow_e));     \
+            return PPG_DEVICE_ERROR;                                                            \
+        }                                                                                       \
+    } while (0)
+
 // waves per candidate range of the block search: enough for ~16,384 waves in all, two generations of
 // the GPU's wave slots (a lone chunk's 48 ranges are searched by 32 waves each; r05: at 4,096 waves a
 // launch of 256 chunks searched its 3,840 ranges with one wave each, 7.0 ms)
@@ -195,6 +212,14 @@ struct ChunkService {
     std::thread worker;
     bool stop = false;
     std::chrono::steady_clock::time_point last_submit{};
+    // the copier of asynchronous results: a launch's async requests are copied out here (holding a
+    // reader on their slot) while the launcher leads the next launch on another slot
+    struct CopyTask {
+        int slot;
+        std::vector<ChunkReq *> reqs;
+    };
+    std::deque<CopyTask> copies;
+    std::thread copier;
 };
 
 ChunkService *chunk_service_new() { return new ChunkService; }
@@ -207,6 +232,7 @@ void chunk_service_free(ChunkService *svc) {
     }
     svc->cv.notify_all();
     if (svc->worker.joinable()) svc->worker.join();
+    if (svc->copier.joinable()) svc->copier.join();   // (it drains the queued copies first)
     for (auto &sl : svc->slot) {
         if (sl.sh) ppg_shard_free(sl.sh);
         if (sl.s) (void)hipStreamDestroy(sl.s);
@@ -558,9 +584,10 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
         for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) jobs[q].bit_limit = ch[c].bit1;
     HIPCHK(grow_buf(F.jobs, np));
     HIPCHK(grow_buf(F.res, np));
-    HIPCHK(grow_buf(F.blk, (size_t)nblk));
-    HIPCHK(grow_buf(F.sym, (size_t)syms + 64));
-    HIPCHK(grow_buf(F.ta, np * 2 * kWin));
+    GROW_OR_SKIP(F.blk, (size_t)nblk);
+    GROW_OR_SKIP(F.sym, (size_t)syms + 64);
+    GROW_OR_SKIP(F.ta, np * 2 * kWin);
+    clk.mark("f.grow");
     if (!F.ident.p) {   // u16 0..32767: position p < 0 of a piece is history symbol 32768 + p
         std::vector<uint16_t> id(kWin);
         for (int i = 0; i < kWin; i++) id[(size_t)i] = (uint16_t)i;
@@ -632,7 +659,7 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     HIPCHK(grow_buf(F.gat, 2 * np));
     HIPCHK(hipMemcpyAsync(F.gat.p, g.data(), sizeof(PpgGather) * 2 * np, hipMemcpyHostToDevice, s));
     HIPCHK(ppg_launch_gather(s, (const uint8_t *)F.sym.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * np)));
-    HIPCHK(grow_buf(F.W, nw * kWin));
+    GROW_OR_SKIP(F.W, nw * kWin);
     HIPCHK(grow_buf(F.slots, nw));
     std::vector<uint32_t> sl_all(nw, 0);
     std::vector<uint4> cs;
@@ -767,6 +794,10 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
         std::vector<std::vector<PpgMatInfo>> pmi;
         std::vector<std::vector<int64_t>> pbit, pout;
         rc = find_mat(sl, (const uint32_t *)sl.comp.p, sh->nwords, sh->dicts.p, find, covered, pmi, pbit, pout, pc);
+        if (rc == PPG_MEM_ERROR) {   // no room for the search's scratch: every chunk decoded whole
+            covered.assign(go.size(), 0);
+            rc = PPG_OK;
+        }
         if (rc != PPG_OK) return rc;
         std::vector<int64_t> sbit, sout;
         size_t ncov = 0;
@@ -906,6 +937,45 @@ bool may_lead(const ChunkService &svc) {
     return !svc.pending.empty() && (svc.in_flight == 0 || svc.pending.size() >= kMinSecond);
 }
 
+using Svc = ChunkService;
+
+// async requests' results into the buffers given at submit, all at once (up to 8 threads); their
+// wait() then only hands back the status and counts
+int copy_async_results(const std::vector<ChunkReq *> &reqs) {
+    try {
+        std::vector<Span> cp;
+        for (ChunkReq *r : reqs)
+            r->fin_rc = result_spans(*r, r->out, r->out_cap, r->recs, r->rec_cap, r->fin_len, r->fin_nrec, cp);
+        parallel_copy(cp);
+    } catch (...) {
+        return PPG_MEM_ERROR;
+    }
+    for (ChunkReq *r : reqs) r->copied = true;
+    return PPG_OK;
+}
+
+// the copier thread (started by the first launch with async requests): drains the copy queue, then
+// exits once the service stops
+void copier_loop(ChunkService *svc) {
+    std::unique_lock<std::mutex> lk(svc->mu);
+    for (;;) {
+        // (a launch still in flight may queue one more task: exit only after it)
+        svc->cv.wait(lk, [&] { return !svc->copies.empty() || (svc->stop && svc->in_flight == 0); });
+        if (svc->copies.empty()) return;
+        Svc::CopyTask t = std::move(svc->copies.front());
+        svc->copies.pop_front();
+        lk.unlock();
+        const int rc = copy_async_results(t.reqs);
+        lk.lock();
+        for (ChunkReq *r : t.reqs) {
+            if (rc != PPG_OK) r->rc = rc;
+            r->done = true;
+        }
+        svc->slot[t.slot].readers--;
+        svc->cv.notify_all();
+    }
+}
+
 // Lead one launch of the queued requests on slot i (lk held on entry and on return, released
 // while the launch runs).  Every request of the batch is marked done; a decoded one holds a reader
 // on the slot until its results are copied out.
@@ -922,28 +992,46 @@ void lead(ppg_ctx *ctx, ChunkService &svc, std::unique_lock<std::mutex> &lk, int
     int rc;
     try {
         rc = run_launch(ctx, svc, sl, batch);
-        if (rc == PPG_OK) {   // async requests: copied out here, all at once, so wait() only hands back
-            std::vector<Span> cp;
-            for (ChunkReq *r : batch)
-                if (r->async && r->rc == PPG_OK)
-                    r->fin_rc = result_spans(*r, r->out, r->out_cap, r->recs, r->rec_cap, r->fin_len, r->fin_nrec, cp);
-            parallel_copy(cp);
-            for (ChunkReq *r : batch) r->copied = r->async && r->rc == PPG_OK;
-        }
     } catch (const std::bad_alloc &) {   // host vectors: never out through the C ABI, never a stuck slot
         rc = PPG_MEM_ERROR;
     } catch (...) {
         rc = PPG_DEVICE_ERROR;
     }
     lk.lock();
+    // async requests go to the copier, which marks them done once their results are in the caller's
+    // buffers (the copies of a 256-chunk launch take about as long as the launch: done here, they
+    // kept the launcher from leading the next one)
+    Svc::CopyTask task{i, {}};
     for (ChunkReq *r : batch) {
         if (rc != PPG_OK) r->rc = rc;
-        if (rc != PPG_OK) r->copied = false;
-        if (r->rc == PPG_OK && !r->copied) {
+        if (r->rc == PPG_OK && r->async) {
+            task.reqs.push_back(r);
+            continue;
+        }
+        if (r->rc == PPG_OK) {
             r->slot = i;
             sl.readers++;
         }
         r->done = true;
+    }
+    if (!task.reqs.empty()) {
+        bool queued = false;
+        try {
+            if (!svc.copier.joinable()) svc.copier = std::thread(copier_loop, &svc);
+            svc.copies.push_back(std::move(task));
+            sl.readers++;   // the copier's
+            queued = true;
+        } catch (...) {
+        }
+        if (!queued) {   // no copier: copy here, the lock released
+            lk.unlock();
+            const int crc = copy_async_results(task.reqs);
+            lk.lock();
+            for (ChunkReq *r : task.reqs) {
+                if (crc != PPG_OK) r->rc = crc;
+                r->done = true;
+            }
+        }
     }
     sl.busy = false;
     svc.in_flight--;
