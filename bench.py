@@ -1153,6 +1153,9 @@ def main():
         # the measured shard (~270 GB of HBM at configs[2]) is done with: the legs below get the device
         del shard, comp
         torch.cuda.empty_cache()
+        # (r05: allocations over the freed HBM are slow for seconds after -- one of 284 GB right
+        # after took 7.9 s, the first multi-GB grow of a launch slot's scratch 3.3-5.6 s; the
+        # per-chunk legs warm every slot first)
     if rank == 0 and world == 1 and args.create_index:
         line["create_index"] = create_index_run(tf, args, dev)
     if rank == 0 and world == 1 and args.ingest:
@@ -1170,6 +1173,8 @@ def main():
             del ictx
             gc.collect()
     if rank == 0 and chunk_legs:
+        free_b, total_b = torch.cuda.mem_get_info(ctx.device)
+        print(f"[bench] chunk legs: {free_b / 1e9:.1f} of {total_b / 1e9:.1f} GB of HBM free", file=sys.stderr, flush=True)
         try:
             line["decompress_chunk"] = decompress_chunk_run(tf, ctx, r["records"])
         except (AssertionError, RuntimeError, pp.PpgError) as e:

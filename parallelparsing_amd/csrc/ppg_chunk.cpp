@@ -8,8 +8,8 @@
 // one of the ctx's four launch slots free takes the queued requests (up to 256) into one launch
 // (flat combining).  A second launch starts beside a running one only once 16 requests queue, so
 // the queue that builds during a launch goes into the next one.  Asynchronous requests
-// (ppg_decompress_chunk_submit) are launched the same way by a launcher thread of the ctx, which
-// also copies their results out.
+// (ppg_decompress_chunk_submit) are launched the same way by a launcher thread of the ctx, and
+// their results copied out by a copier thread while the next launch runs.
 //
 // A slot owns everything a launch touches -- its stream, a one-batch ppg_shard, the gathered
 // compressed slices (pinned + device), the pinned copy of the outputs and descriptors, the block
@@ -58,6 +58,11 @@ constexpr size_t kMaxBatch = 256;
 // queue grows during the running launch and the next one takes all of it (r04: with two slots taken
 // as soon as free, 64 callers were served ~12 at a time)
 constexpr size_t kMinSecond = 16;
+// launcher threads of asynchronous requests.  r05 (tools/chunk_latency.py, async depth 1024, three
+// runs): one 19 / 31 / 39 M records/s, two 16 / 18 / 30 -- the second overlaps a launch's PCIe
+// copies with the other's kernels, but the two launches' host copies (slices gathered, results
+// copied out into fresh pages) then contend, and more slots are grown
+constexpr int kLaunchers = 1;
 
 struct ChunkReq {
     const ppg_index *ix;
@@ -209,7 +214,7 @@ struct ChunkService {
     std::atomic<int64_t> found_chunks{0}, found_points{0};   // find_side_points' splits
     // the launcher of asynchronous requests (started by the first ppg_decompress_chunk_submit)
     ppg_ctx *ctx = nullptr;
-    std::thread worker;
+    std::thread worker[kLaunchers];
     bool stop = false;
     std::chrono::steady_clock::time_point last_submit{};
     // the copier of asynchronous results: a launch's async requests are copied out here (holding a
@@ -231,7 +236,8 @@ void chunk_service_free(ChunkService *svc) {
         svc->stop = true;
     }
     svc->cv.notify_all();
-    if (svc->worker.joinable()) svc->worker.join();
+    for (auto &w : svc->worker)
+        if (w.joinable()) w.join();
     if (svc->copier.joinable()) svc->copier.join();   // (it drains the queued copies first)
     for (auto &sl : svc->slot) {
         if (sl.sh) ppg_shard_free(sl.sh);
@@ -563,6 +569,12 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     }
     const size_t np = pc.size();
     if (!np) return PPG_OK;
+    // a repair piece per chunk at most (below): its symbols, block ends and job reserved up front
+    // (grow_buf does not keep contents, and a hipFree mid-launch waits for the whole device)
+    uint64_t maxcap = 0;
+    for (const MatPiece &m : pc) maxcap = std::max(maxcap, m.cap);
+    const size_t nrep_cap = ch.size();
+    const uint64_t rep_syms = std::max<uint64_t>(4 * (maxcap + 2048), syms / 16);
     std::vector<PpgInflateJob> jobs(np);
     uint64_t nblk = 0;
     for (size_t q = 0; q < np; q++) {
@@ -578,15 +590,16 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
         J.blk_cap = (uint32_t)((pc[q].stop - pc[q].start) / 8 / 2048 + 64);
         nblk += J.blk_cap;
     }
+    const uint64_t rep_blk = 64 * nrep_cap + rep_syms / (kMatRatio * 2048) + 64;
     // the piece may read up to its chunk's slice end (the last block of a non-final piece ends past
     // its stop when the next candidate was false)
     for (size_t c = 0; c < ch.size(); c++)
         for (size_t q = pfirst[c]; q < pfirst[c + 1]; q++) jobs[q].bit_limit = ch[c].bit1;
-    HIPCHK(grow_buf(F.jobs, np));
-    HIPCHK(grow_buf(F.res, np));
-    GROW_OR_SKIP(F.blk, (size_t)nblk);
-    GROW_OR_SKIP(F.sym, (size_t)syms + 64);
-    GROW_OR_SKIP(F.ta, np * 2 * kWin);
+    HIPCHK(grow_buf(F.jobs, np + nrep_cap));
+    HIPCHK(grow_buf(F.res, np + nrep_cap));
+    GROW_OR_SKIP(F.blk, (size_t)(nblk + rep_blk));
+    GROW_OR_SKIP(F.sym, (size_t)(syms + rep_syms) + 64);
+    GROW_OR_SKIP(F.ta, (np + nrep_cap) * 2 * kWin);
     clk.mark("f.grow");
     if (!F.ident.p) {   // u16 0..32767: position p < 0 of a piece is history symbol 32768 + p
         std::vector<uint16_t> id(kWin);
@@ -607,40 +620,136 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     // candidate (its piece fails, or the piece before it decodes on to the next real block end) the
     // first later piece that starts there, the false ones skipped (r05: ~0.6% of chunks at 48
     // ranges fell back to a one-wave decode of ~45 ms) --, the chain's last piece ends exactly at
-    // the chunk's end (or with the final block, for the file's last chunk), and their outputs add up
+    // the chunk's end (or with the final block, for the file's last chunk), and their outputs add up.
+    // Two more cases chain (r05: 2 chunks in 1,024 were still left to the one-wave decode):
+    //  - the real block start after a false candidate is no candidate at all (the finder keeps one
+    //    per range): a repair piece from that block end to the next good piece's start, decoded in
+    //    a second, small pass 1;
+    //  - an index's last chunk, whose end is known only as its slice's last byte (no R-E5 end check:
+    //    expect_end ~0): its last piece ends a block inside that byte, with every byte of the chunk,
+    //    and decodes on into a next block header the slice does not hold, failing -- the piece is
+    //    taken up to that block end (r05: index chunk 1023 of the bench's per-chunk legs).
     std::vector<size_t> wbase(ch.size(), 0);
     std::vector<std::vector<uint32_t>> chain(ch.size());
     std::vector<uint64_t> E(np, 0);
-    size_t nw = 0;
-    for (size_t c = 0; c < ch.size(); c++) {
+    std::vector<uint8_t> cut(np, 0);                      // last pieces taken up to a block end in the slice's last byte
+    std::vector<std::vector<uint32_t>> reps(ch.size());   // each chunk's repair pieces (indexes >= np)
+    struct Repair {
+        size_t c;
+        uint64_t start, stop;
+    };
+    std::vector<Repair> want;
+    // chunk c's chain; 0 when covered, else why not (PPG_CHUNK_VERBOSE)
+    auto walk = [&](size_t c, bool may_repair) -> int {
+        chain[c].clear();
         uint64_t tot = 0;
-        int why = 0;   // (PPG_CHUNK_VERBOSE: why a chunk is not covered)
-        bool done = false;
         size_t q = pfirst[c];
-        while (q < pfirst[c + 1]) {
-            const PpgInflateResult &r = res[q];
+        for (;;) {
+            PpgInflateResult &r = res[q];
             const uint32_t nb = std::min(r.nblocks, jobs[q].blk_cap);
-            if (r.status != 0 || nb == 0 || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN))) {
-                why = r.status != 0 ? 1 : nb == 0 ? 2 : (r.flags & PPG_FLAG_BLK_FULL) ? 3 : 4;
-                break;
+            if (r.status != 0 && nb > 0 && ch[c].bit_end == ch[c].bit1) {   // an index's last chunk
+                const PpgBlockEnd &e = blk[jobs[q].blk_off + nb - 1];
+                if (e.end_bit <= ch[c].bit_end && ch[c].bit_end - e.end_bit < 8 &&
+                    tot + e.out_end == (uint64_t)ch[c].len && e.out_end <= jobs[q].out_len) {
+                    r.status = 0;
+                    r.flags = 0;
+                    r.produced = e.out_end;
+                    r.nblocks = nb;
+                    r.last = 0;
+                    cut[q] = 1;
+                }
             }
+            if (r.status != 0 || nb == 0 || (r.flags & (PPG_FLAG_BLK_FULL | PPG_FLAG_OVERRUN)))
+                return r.status != 0 ? 1 : nb == 0 ? 2 : (r.flags & PPG_FLAG_BLK_FULL) ? 3 : 4;
             const PpgBlockEnd &e = blk[jobs[q].blk_off + nb - 1];
-            if (e.out_end != r.produced) { why = 5; break; }
+            if (e.out_end != r.produced) return 5;
             E[q] = e.end_bit;
             chain[c].push_back((uint32_t)q);
             tot += r.produced;
-            if (e.end_bit == ch[c].bit_end || (r.last && ch[c].bit_end == ch[c].bit1)) { done = true; break; }
-            if (r.last) { why = 6; break; }
-            size_t nx = q + 1;   // the piece that starts at this end
+            if (e.end_bit == ch[c].bit_end || cut[q] || (r.last && ch[c].bit_end == ch[c].bit1))
+                return (int64_t)tot == ch[c].len ? 0 : 9;
+            if (r.last) return 6;
+            size_t nx = q < np ? q + 1 : pfirst[c];   // the piece that starts at this end
             while (nx < pfirst[c + 1] && pc[nx].start < e.end_bit) nx++;
-            if (nx >= pfirst[c + 1] || pc[nx].start != e.end_bit) { why = 7; break; }
-            q = nx;
+            if (nx < pfirst[c + 1] && pc[nx].start == e.end_bit) {
+                q = nx;
+                continue;
+            }
+            size_t rq = ~(size_t)0;
+            for (uint32_t x : reps[c])
+                if (pc[x].start == e.end_bit) rq = x;
+            if (rq != ~(size_t)0) {
+                q = rq;
+                continue;
+            }
+            if (may_repair) {   // up to the next piece that decoded, or the chunk's end
+                while (nx < pfirst[c + 1] && res[nx].status != 0) nx++;
+                want.push_back(Repair{c, e.end_bit, nx < pfirst[c + 1] ? pc[nx].start : ch[c].bit_end});
+            }
+            return 7;
         }
-        if (done && (int64_t)tot != ch[c].len) why = 9;
-        const bool ok = done && (int64_t)tot == ch[c].len;
-        if (!ok && clk.on)
-            fprintf(stderr, "PPG_CHUNK not covered: chunk %zu reason %d after %zu chained of %zu pieces\n", c, why,
+    };
+    std::vector<int> why(ch.size(), 0);
+    for (size_t c = 0; c < ch.size(); c++) why[c] = walk(c, true);
+    if (!want.empty()) {   // the repair pass
+        uint64_t rs = syms, rb = nblk;
+        std::vector<size_t> rc;
+        for (const Repair &w : want) {
+            const uint64_t cap = std::max<uint64_t>(192 * 1024, kMatRatio * ((w.stop - w.start) / 8 + 64));
+            const uint32_t bc = (uint32_t)((w.stop - w.start) / 8 / 2048 + 64);
+            if (w.stop <= w.start || rs + cap + 2048 > syms + rep_syms || rb + bc > nblk + rep_blk) continue;
+            PpgInflateJob J{};
+            J.bit_start = w.start;
+            J.bit_limit = ch[w.c].bit1;
+            J.out_off = rs;
+            J.out_len = cap;
+            J.expect_end = ~0ull;
+            J.stop_bit = w.stop;
+            J.blk_off = (uint32_t)rb;
+            J.blk_cap = bc;
+            reps[w.c].push_back((uint32_t)pc.size());
+            pc.push_back(MatPiece{w.start, w.stop, rs, cap});
+            jobs.push_back(J);
+            rc.push_back(w.c);
+            rs += cap + 2048;
+            rb += bc;
+        }
+        const size_t nr = pc.size() - np;
+        if (nr) {
+            res.resize(np + nr);
+            blk.resize((size_t)rb);
+            E.resize(np + nr, 0);
+            cut.resize(np + nr, 0);
+            HIPCHK(hipMemcpyAsync(F.jobs.p + np, jobs.data() + np, sizeof(PpgInflateJob) * nr, hipMemcpyHostToDevice, s));
+            HIPCHK(ppg_launch_inflate_ixf(s, comp, nwords, F.jobs.p + np, F.ident.p, (uint8_t *)F.sym.p, F.res.p + np,
+                                          F.blk.p, (int)nr));
+            HIPCHK(hipMemcpyAsync(res.data() + np, F.res.p + np, sizeof(PpgInflateResult) * nr, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(blk.data() + nblk, F.blk.p + nblk, sizeof(PpgBlockEnd) * (rb - nblk),
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            std::sort(rc.begin(), rc.end());
+            rc.erase(std::unique(rc.begin(), rc.end()), rc.end());
+            for (size_t c : rc) why[c] = walk(c, false);
+        }
+        clk.mark("f.repair");
+    }
+    const size_t nt = pc.size();
+    size_t nw = 0;
+    for (size_t c = 0; c < ch.size(); c++) {
+        const bool ok = why[c] == 0;
+        if (!ok && clk.on) {
+            fprintf(stderr, "PPG_CHUNK not covered: chunk %zu reason %d after %zu chained of %zu pieces\n", c, why[c],
                     chain[c].size(), pfirst[c + 1] - pfirst[c]);
+            for (size_t x = pfirst[c]; x < pfirst[c + 1]; x++) {
+                const PpgInflateResult &r = res[x];
+                const uint32_t nb = std::min(r.nblocks, jobs[x].blk_cap);
+                fprintf(stderr, "  piece %zu bits [%llu,%llu) chunk [%llu,%llu) cap %llu: status %d flags %u produced %llu "
+                        "blocks %u last_end %llu\n", x - pfirst[c], (unsigned long long)pc[x].start,
+                        (unsigned long long)pc[x].stop, (unsigned long long)ch[c].bit0, (unsigned long long)ch[c].bit_end,
+                        (unsigned long long)pc[x].cap, (int)r.status, (unsigned)r.flags, (unsigned long long)r.produced, nb,
+                        nb ? (unsigned long long)blk[jobs[x].blk_off + nb - 1].end_bit : 0ull);
+            }
+        }
         covered[c] = ok;
         if (ok) {
             wbase[c] = nw;
@@ -650,15 +759,15 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
     if (!nw) return PPG_OK;
     // symbolic tails (the last 32 Ki symbols of each piece, as two 32 KiB byte halves), then every
     // covered chunk's starting histories: W[0] = the Point's window, W[j+1] = T_j(W[j])
-    std::vector<PpgGather> g(2 * np);
-    for (size_t q = 0; q < np; q++) {
+    std::vector<PpgGather> g(2 * nt);
+    for (size_t q = 0; q < nt; q++) {
         const uint64_t endb = 2 * res[q].produced, base = 2 * pc[q].sym_off;
         g[2 * q] = PpgGather{base, (uint64_t)kWin, endb - kWin, ~0ull, 0};
         g[2 * q + 1] = PpgGather{base, (uint64_t)kWin, endb, ~0ull, 0};
     }
-    HIPCHK(grow_buf(F.gat, 2 * np));
-    HIPCHK(hipMemcpyAsync(F.gat.p, g.data(), sizeof(PpgGather) * 2 * np, hipMemcpyHostToDevice, s));
-    HIPCHK(ppg_launch_gather(s, (const uint8_t *)F.sym.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * np)));
+    HIPCHK(grow_buf(F.gat, 2 * nt));
+    HIPCHK(hipMemcpyAsync(F.gat.p, g.data(), sizeof(PpgGather) * 2 * nt, hipMemcpyHostToDevice, s));
+    HIPCHK(ppg_launch_gather(s, (const uint8_t *)F.sym.p, F.ident.p, F.gat.p, F.ta.p, nullptr, nullptr, (int)(2 * nt)));
     GROW_OR_SKIP(F.W, nw * kWin);
     HIPCHK(grow_buf(F.slots, nw));
     std::vector<uint32_t> sl_all(nw, 0);
@@ -965,7 +1074,14 @@ void copier_loop(ChunkService *svc) {
         Svc::CopyTask t = std::move(svc->copies.front());
         svc->copies.pop_front();
         lk.unlock();
+        PhaseClock clk;
         const int rc = copy_async_results(t.reqs);
+        if (clk.on) {
+            int64_t b = 0;
+            for (ChunkReq *r : t.reqs) b += r->fin_len + 16 * (r->recs ? r->nrec : 0);
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - clk.t0).count();
+            fprintf(stderr, "PPG_CHUNK copy of %zu: %.1f MB in %.3f ms (slot %d)\n", t.reqs.size(), b / 1e6, ms, t.slot);
+        }
         lk.lock();
         for (ChunkReq *r : t.reqs) {
             if (rc != PPG_OK) r->rc = rc;
@@ -1124,13 +1240,19 @@ int ppg_decompress_chunk_submit(ppg_ctx *ctx, const ppg_index *ix, int32_t k, co
     r->rec_cap = rec_cap;
     {
         std::lock_guard<std::mutex> lk(svc->mu);
-        if (!svc->worker.joinable()) {
+        if (!svc->worker[0].joinable()) {
             svc->ctx = ctx;
             try {
-                svc->worker = std::thread(worker_loop, svc);
+                svc->worker[0] = std::thread(worker_loop, svc);
             } catch (...) {
                 delete r;
                 return PPG_MEM_ERROR;
+            }
+            for (int w = 1; w < kLaunchers; w++) {   // (more launchers are an optimisation only)
+                try {
+                    svc->worker[w] = std::thread(worker_loop, svc);
+                } catch (...) {
+                }
             }
         }
         svc->calls++;
