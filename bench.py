@@ -18,7 +18,6 @@ consumer enumerating records would.
   N > 1 defaults to strong scaling: one ~50 GB member split over the N GPUs (configs[3]).
 """
 import argparse
-import gc
 import json
 import os
 import socket
@@ -369,7 +368,14 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
     plain = tf.index(0, nmax + 1)
     split = tf.index(0, nmax + 1).set_side_points(*tf.side_points(0, nmax + 1, side))
 
-    def leg(ix, T):
+    def leg(ix, T, runs=1):
+        """T threads (one untimed run first and the median of `runs` when runs > 1: HBM freed just
+        before the legs -- the ingest's pieces, the shard -- is cleared by the driver for seconds
+        after, and the clearing shares the copy engines with the launches' H2D/D2H; r05: one T = 64
+        run read 23 M records/s there, 36-42 M in other runs)."""
+        if runs > 1:
+            leg(ix, T)
+            return sorted((leg(ix, T) for _ in range(runs)), key=lambda r: r["records_per_s"])[runs // 2]
         n = min(nmax, per_thread * T)
         before = dev.decompress_chunk_stats()
         nxt = [0]
@@ -438,13 +444,13 @@ def decompress_chunk_run(tf, dev, counts, threads_list=(1, 8, 64), per_thread=16
     # warm: the launcher thread, and the launch slots' buffers grown to full launches (256 chunks each)
     async_once(plain, nmax)
     leg(plain, 8)
-    out = {f"T{T}": leg(plain, T) for T in threads_list}
+    out = {f"T{T}": leg(plain, T, runs=3) for T in threads_list}
     out["async"] = {f"depth{d}": async_leg(plain, d) for d in (256, 1024)}
     out["no_find"] = {f"T{T}": no_find(T) for T in threads_list}
     out["side_points"] = {f"T{T}": leg(split, T) for T in threads_list}
     out["note"] = ("ppg_decompress_chunk from T host threads on one ctx (concurrent calls combined into shared "
                    "launches, four launch slots); async: one thread queues `depth` chunks (ppg_decompress_chunk_submit) "
-                   "then waits for each; plain index: each chunk's inner block starts found on the GPU "
+                   "then waits for each; plain index and async: median of 3 after an untimed run; plain index: each chunk's inner block starts found on the GPU "
                    "(<= 16 waves per chunk); no_find: one wave per chunk; side_points: the index's own, "
                    f"<= {side} waves per chunk (ppg_index_set_side_points); host slices in, bytes + descriptors out; "
                    "not the bench value")
@@ -1159,19 +1165,18 @@ def main():
     if rank == 0 and world == 1 and args.create_index:
         line["create_index"] = create_index_run(tf, args, dev)
     if rank == 0 and world == 1 and args.ingest:
-        # a ctx of its own: its ingest buffers (three 8 GiB pieces and their shards' outputs) are
-        # freed with it, before the per-chunk legs
-        ictx = pp.Device(ctx.device)
+        # on the bench's own ctx (r05: a second ctx measured 345 against 398 M records/s, one box,
+        # profiles/r05zv_ingest_ctx.txt); its buffers -- three 8 GiB pieces and their shards'
+        # outputs -- are freed after it (ppg_file_release), before the per-chunk legs
         try:
-            line["ingest"], enum = ingest_run(tf, tf.index(0, tf.npoints), ictx, args.host_threads,
+            line["ingest"], enum = ingest_run(tf, tf.index(0, tf.npoints), ctx, args.host_threads,
                                               args.ingest_piece_gib, 0 if args.no_enumerate else args.enum_batch_gib)
             if enum is not None:
                 line["enumerate"] = enum
         except (OSError, AssertionError, RuntimeError) as e:   # e.g. no room for the file in $TMPDIR
             line["ingest"] = {"error": f"{type(e).__name__}: {e}"}
         finally:
-            del ictx
-            gc.collect()
+            ctx.release_file_buffers()
     if rank == 0 and chunk_legs:
         free_b, total_b = torch.cuda.mem_get_info(ctx.device)
         print(f"[bench] chunk legs: {free_b / 1e9:.1f} of {total_b / 1e9:.1f} GB of HBM free", file=sys.stderr, flush=True)

@@ -262,6 +262,11 @@ int ppg_shard_timing(ppg_shard *sh, float *inflate_ms, float *parse_ms, float *t
 int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
                             int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,
                             double *seconds);
+/* Frees the buffers ppg_file_decompress_all keeps in the ctx (its device pieces and their shards'
+ * outputs, tens of GB at 8 GiB pieces; the pinned staging; its streams) -- e.g. before other work
+ * needs the HBM; the next call allocates them again.  Not while a ppg_file_decompress_all runs on
+ * the ctx.  Returns 0, or PPG_ARG_ERROR for a NULL ctx. */
+int ppg_file_release(ppg_ctx *ctx);
 
 /* ======================= streamed records: BatchedFASTQ's enumerator =======================
  * Decompressor/BatchedFASTQ.cs:29-101 (IEnumerable<FastqRecord> over a bounded record cache fed by

@@ -134,6 +134,7 @@ internal static unsafe class PpGpu
     // ---- LazyFileReader (LazyFileReader.cs:10-98): DecompressAll straight from the file ----
     [DllImport(Lib)] public static extern int ppg_file_decompress_all(nint ctx, nint ix, string gzPath, int first,
         int n, long pieceBytes, int threads, long* records, out long totalRecords, out double seconds);
+    [DllImport(Lib)] public static extern int ppg_file_release(nint ctx);
 
     // ---- BatchedFASTQ's enumerator (BatchedFASTQ.cs:29-101): streamed record batches ----
     [DllImport(Lib)] public static extern int ppg_cursor_open(nint ctx, nint ix, string gzPath, int first, int n,

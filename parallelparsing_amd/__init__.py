@@ -193,6 +193,11 @@ class Device:
         """Order `stream`'s later work after everything queued on this ctx so far (ppg_stream_wait_ctx)."""
         check(lib.ppg_stream_wait_ctx(self._h, C.c_void_p(_stream_handle(stream))), "ppg_stream_wait_ctx")
 
+    def release_file_buffers(self):
+        """Free what decompress_file keeps in this ctx between calls (ppg_file_release): its device
+        pieces and their shards' outputs, the pinned staging; the next call allocates them again."""
+        check(lib.ppg_file_release(self._h), "ppg_file_release")
+
     def decompress_chunk_stats(self):
         """{calls, launches, max_batch, split_chunks, side_points} of ppg_decompress_chunk on this
         ctx: how the thread-safe per-chunk Decompress combined concurrent calls into launches, and

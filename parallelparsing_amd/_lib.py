@@ -110,6 +110,7 @@ _SIGS = {
     "ppg_shard_counts_to_device": (C.c_int, [vp, vp]),
     "ppg_shard_timing": (C.c_int, [vp, P(C.c_float), P(C.c_float), P(C.c_float)]),
     "ppg_file_decompress_all": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, vp, P(i64), P(C.c_double)]),
+    "ppg_file_release": (C.c_int, [vp]),
     "ppg_version": (C.c_char_p, []),
     "ppg_build_id": (C.c_char_p, []),
     "ppg_cursor_open": (C.c_int, [vp, vp, C.c_char_p, i32, i32, i64, C.c_int, P(vp)]),

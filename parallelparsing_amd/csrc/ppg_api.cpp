@@ -1101,6 +1101,16 @@ int shard_split_from_index(ppg_shard *sh, const ppg_index *ix, int32_t first, in
 
 extern "C" {
 
+int ppg_file_release(ppg_ctx *ctx) {
+    if (!ctx) return PPG_ARG_ERROR;
+    if (ctx->ingest) {
+        HIPCHK(hipSetDevice(ctx->device));
+        ingest_free(ctx->ingest);
+        ctx->ingest = nullptr;
+    }
+    return PPG_OK;
+}
+
 int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_path, int32_t first, int32_t n,
                             int64_t piece_bytes, int threads, int64_t *records, int64_t *total_records,
                             double *seconds) {

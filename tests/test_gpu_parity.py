@@ -201,6 +201,11 @@ def test_file_ingest_matches_golden(name, piece, tmp_path, device):
     if ix.Count > 4:
         rec2, tot2, _ = pp.decompress_file(ix, str(p), first=1, n=ix.Count - 3, piece_bytes=piece, device=device)
         assert [int(x) for x in rec2] == [c["records"] for c in meta["chunks"][1:ix.Count - 2]]
+    # the kept buffers freed (ppg_file_release, twice: a no-op the second time), then allocated again
+    device.release_file_buffers()
+    device.release_file_buffers()
+    rec3, tot3, _ = pp.decompress_file(ix, str(p), piece_bytes=piece, threads=2, device=device)
+    assert [int(x) for x in rec3] == [c["records"] for c in meta["chunks"]] and tot3 == tot
 
 
 def test_file_ingest_errors(tmp_path, device):
