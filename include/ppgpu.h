@@ -164,10 +164,13 @@ int ppg_decompress_chunk(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uin
 /* The same, asynchronous: one caller keeps many chunks in flight, as the reference's reader keeps 32
  * partitions queued (LazyFileReader.cs:14) for its tasks.  submit queues the request and returns a
  * ticket at once; a launcher thread of the ctx (started by the first submit) combines the queued
- * requests -- a burst of submissions goes into one launch of up to 256 chunks --, copies each
- * decoded chunk's bytes / records into the buffers given at submit (up to 8 threads per launch), and
- * ppg_decompress_chunk_wait blocks until that is done, returns the status and counts, and frees the
- * ticket (slice, out and recs must stay valid until then).  Every ticket must be waited for, each once, on the ctx it was submitted to. */
+ * requests -- a burst of submissions goes into one launch of up to 256 chunks --, a copier thread
+ * copies each decoded chunk's bytes / records into the buffers given at submit (up to 8 threads per
+ * launch) while the next launch runs, and ppg_decompress_chunk_wait blocks until that is done,
+ * returns the status and counts, and frees the ticket (slice, out and recs must stay valid until
+ * then).  Every ticket must be waited for, each once, on the ctx it was submitted to.  (Both forms:
+ * where results of a launch are copied out together, the whole 2 MiB pages inside each caller
+ * buffer get madvise(MADV_HUGEPAGE) first -- advice only, the copy is ~2x faster into fresh pages.) */
 typedef struct ppg_chunk_req ppg_chunk_req;
 int ppg_decompress_chunk_submit(ppg_ctx *ctx, const ppg_index *ix, int32_t k, const uint8_t *slice, int64_t slice_len,
                                 uint8_t *out, int64_t out_cap, uint32_t *recs, int64_t rec_cap, ppg_chunk_req **req);
