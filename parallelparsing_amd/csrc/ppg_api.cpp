@@ -318,7 +318,7 @@ int ppg_index_validate(const ppg_index *ix, int32_t first, int32_t n) {
     return PPG_OK;
 }
 
-const char *ppg_version(void) { return "ppgpu 0.3 gfx950 (wave-per-chunk inflate, 1 KiB LDS history ring, fused newline census)"; }
+const char *ppg_version(void) { return "ppgpu 0.3 gfx950 (wave-per-chunk inflate, 2 KiB LDS history ring, fused newline census)"; }
 
 }  // extern "C"
 
@@ -359,7 +359,7 @@ int ppg_open(int device, ppg_ctx **out) {
     ctx->chunks = chunk_service_new();
     if (const char *rb = getenv("PPG_RING_BITS")) ctx->ring_bits = std::min(15, std::max(10, atoi(rb)));
     if (const char *lb = getenv("PPG_LIT_BITS")) ctx->lit_bits = std::min(9, std::max(8, atoi(lb)));
-    if (ppg_inflate_lds_bytes(ctx->ring_bits, ctx->lit_bits) == 0) { ctx->ring_bits = 10; ctx->lit_bits = 8; }
+    if (ppg_inflate_lds_bytes(ctx->ring_bits, ctx->lit_bits) == 0) { ctx->ring_bits = 11; ctx->lit_bits = 8; }
     *out = ctx.release();
     return PPG_OK;
 }

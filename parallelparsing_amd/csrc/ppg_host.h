@@ -107,7 +107,7 @@ struct ppg_ctx {
     hipEvent_t handoff = nullptr;   // ppg_ctx_wait_stream / ppg_stream_wait_ctx
     IngestState *ingest = nullptr;
     ChunkService *chunks = nullptr;
-    int ring_bits = 10;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (1 KiB: 32 waves/CU)
+    int ring_bits = 11;   // inflate history ring: 2^10..2^15 bytes of LDS per wavefront (2 KiB: 32 waves/CU)
     int lit_bits = 8;     // litlen root table: 2^8 entries (codes <= 8 bits: 99.65% of FASTQ tokens)
     double ix_stats[kIxStats] = {0};   // timings / counts of the last GPU CreateIndex (ppg_index_build_gpu_stats)
     uint8_t *stage = nullptr;           // pinned device -> host staging (CreateIndex windows), kept across calls

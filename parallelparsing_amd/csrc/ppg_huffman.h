@@ -74,9 +74,11 @@ struct Canon {
     uint32_t count, first, index;
 };
 
+// copy_to (may be NULL): where the sorted symbols are kept for canon_decode when `sorted` is only
+// LDS scratch of the build (ppg_inflate_kernel, PPG_GSORT: global memory, written once per table)
 template <int TB>
 __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, Canon *canon, uint16_t *sorted, int kind,
-                           int lane) {
+                           int lane, uint16_t *copy_to = nullptr) {
     // Runs once per block, so it is written for few registers, not speed: per-length counts,
     // offsets and running ranks live one per lane (lane l holds length l), loops stay rolled.
     uint32_t cnt = 0;
@@ -145,6 +147,8 @@ __device__ int build_table(const uint8_t *lens, int n, uint32_t *table, Canon *c
         }
         table[e] = entry;
     }
+    if (copy_to)
+        for (int i = lane; i < n; i += 64) copy_to[i] = sorted[i];
     __syncthreads();
     return 0;
 }

@@ -30,6 +30,8 @@
 #include <type_traits>
 #include "ppg_device.h"
 #include "ppg_huffman.h"
+#include <atomic>
+#define PPG_SORT_SLOT 320   // u16 per wave in global scratch: litlen sorted symbols 288, distance 32
 
 // CreateIndex pass 1 (IX): each job's output lives in a ring of 64 Ki positions of the out buffer
 // (only the last 32 KiB + REACH are ever read back).  Pass 1 does not know a piece's starting
@@ -61,11 +63,7 @@ struct __attribute__((aligned(16))) InflateLds {
         uint32_t cl[1 << CB];
     };
     uint32_t dst[1 << DB];
-    union {
-        uint16_t lit_sorted[288];
-        uint16_t cl_sorted[20];
-    };
-    uint16_t dst_sorted[32];
+    // (the canonical codes' sorted symbols are in global scratch: see ppg_inflate_kernel)
     uint8_t lens[320];
     uint32_t cen[8];               // newline census: count, previous byte was '\n', PPG_PF_* flags, cap, shift, dst
 };
@@ -537,7 +535,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                                                          const PpgInflateJob *__restrict__ jobs,
                                                          const uint8_t *__restrict__ dicts, uint8_t *__restrict__ out,
                                                          PpgInflateResult *__restrict__ res, int njobs,
-                                                         PpgBlockEnd *__restrict__ blk, uint32_t *__restrict__ nls) {
+                                                         PpgBlockEnd *__restrict__ blk, uint32_t *__restrict__ nls,
+                                                         uint16_t *__restrict__ gsort) {
     constexpr uint32_t RING = 1u << RB;
     constexpr uint32_t RM = RING - 1;
     // flush unit: far references (older than REACH = RING - 64) must already be flushed; a round
@@ -553,6 +552,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     const int lane = threadIdx.x;
     const int k = blockIdx.x;
     if (k >= njobs) return;
+    // The canonical codes' sorted symbols (for the bit-serial path: long codes, end-of-block) live
+    // in global scratch, PPG_SORT_SLOT per wave: their 640 B of LDS now hold a 2 KiB history ring
+    // at 8 waves per SIMD (InflateLds<11, 8>: 4,976 B of the 5,120 a wave gets).  A table build
+    // sorts into LDS that is free at that moment -- the distance table's for the litlen and
+    // code-length codes, the dead code lengths' head for the distance code -- and copies the
+    // result out once.  r05, one same-box A/B of the 50 GB step (profiles/r05zzb_ab_gsort.json):
+    // 555.2 ms (1 KiB ring, sorted symbols in LDS) -> 533.3; the global sorted symbols alone (1 KiB
+    // ring) 565.2, sorting straight into global memory 562.8 / 540.4 (r05zza).
+    uint16_t *const lit_sorted = gsort + (size_t)k * PPG_SORT_SLOT;
+    uint16_t *const dst_sorted = lit_sorted + 288;
+    uint16_t *const lit_tmp = (uint16_t *)S.dst, *const cl_tmp = (uint16_t *)S.dst, *const dst_tmp = (uint16_t *)S.lens;
     const PpgInflateJob J = jobs[k];
     const uint64_t out_off = J.out_off;
     const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // < 2^31: ppg_index_validate
@@ -711,8 +721,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 S.lens[s] = L;
             }
             __syncthreads();
-            build_table<LBT>(S.lens, 288, S.lit, &clit, S.lit_sorted, TAB_LIT, lane);
-            build_table<DB>(S.lens + 288, 32, S.dst, &cdst, S.dst_sorted, TAB_DST, lane);
+            build_table<LBT>(S.lens, 288, S.lit, &clit, lit_tmp, TAB_LIT, lane, lit_sorted);
+            build_table<DB>(S.lens + 288, 32, S.dst, &cdst, dst_tmp, TAB_DST, lane, dst_sorted);
         } else {
             // ---- dynamic Huffman codes (RFC 1951 3.2.7) ----
             asm volatile("s_setprio 2");
@@ -727,7 +737,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if (lane == 0) S.lens[c_clorder[i]] = (uint8_t)v;
             }
             __syncthreads();
-            if (build_table<CB>(S.lens, 19, S.cl, nullptr, S.cl_sorted, TAB_CL, lane) != 0) { status = ST_DATA_ERROR; break; }
+            if (build_table<CB>(S.lens, 19, S.cl, nullptr, cl_tmp, TAB_CL, lane) != 0) { status = ST_DATA_ERROR; break; }
             uint32_t idx = 0;
             const uint32_t total = hlit + hdist;
             bool bad = false;
@@ -754,8 +764,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             __syncthreads();
             if (bad) { status = ST_DATA_ERROR; break; }
             if (uni(S.lens[256]) == 0) { status = ST_DATA_ERROR; break; }   // no end-of-block code
-            if (build_table<LBT>(S.lens, (int)hlit, S.lit, &clit, S.lit_sorted, TAB_LIT, lane) != 0) { status = ST_DATA_ERROR; break; }
-            if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, &cdst, S.dst_sorted, TAB_DST, lane) != 0) { status = ST_DATA_ERROR; break; }
+            if (build_table<LBT>(S.lens, (int)hlit, S.lit, &clit, lit_tmp, TAB_LIT, lane, lit_sorted) != 0) { status = ST_DATA_ERROR; break; }
+            if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, &cdst, dst_tmp, TAB_DST, lane, dst_sorted) != 0) { status = ST_DATA_ERROR; break; }
         }
         in_block = 1;
         asm volatile("s_setprio 0");
@@ -1155,7 +1165,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             asm volatile("s_setprio 2");
             rd_seek(r, S.stream, bp, lane);
             rd_refill(r, S.stream, lane);
-            const int sym = canon_decode(r, clit, S.lit_sorted, lane);
+            const int sym = canon_decode(r, clit, lit_sorted, lane);
 #ifdef PPG_STATS
             if (sym < 256) st_blit++; else if (sym == 256) st_beob++; else st_bmatch++;
 #endif
@@ -1170,7 +1180,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             } else {
                 const uint32_t ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
                 rd_refill(r, S.stream, lane);
-                const int dsym = canon_decode(r, cdst, S.dst_sorted, lane);
+                const int dsym = canon_decode(r, cdst, dst_sorted, lane);
                 if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
                 const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
                 const uint32_t n = min(ml, len - pos);
@@ -1206,7 +1216,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     }
     if (!IX && status == ST_OK && in_block && pos == len) {
         rd_refill(r, S.stream, lane);
-        if (canon_decode(r, clit, S.lit_sorted, lane) == 256) end_bit = rd_pos(r);
+        if (canon_decode(r, clit, lit_sorted, lane) == 256) end_bit = rd_pos(r);
         else flags |= PPG_FLAG_NO_EOB;
     }
 #ifdef PPG_STATS
@@ -1256,10 +1266,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     }
 }
 
+// per-launch scratch of the sorted-symbol tables, stream-ordered: no device-wide sync, and the
+// device's default pool keeps the memory between launches (release threshold raised once)
+static hipError_t gsort_alloc(hipStream_t s, int njobs, uint16_t **p) {
+    static std::atomic<uint64_t> pools_set{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 64 && !(pools_set.load() >> dev & 1)) {
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t t = ~0ull;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &t);
+        }
+        pools_set.fetch_or(1ull << dev);
+    }
+    return hipMallocAsync((void **)p, (size_t)njobs * PPG_SORT_SLOT * sizeof(uint16_t), s);
+}
+#define PPG_GSORT_BEGIN(s, njobs)                          \
+    uint16_t *gsort = nullptr;                             \
+    {                                                      \
+        const hipError_t ge = gsort_alloc(s, njobs, &gsort); \
+        if (ge != hipSuccess) return ge;                   \
+    }
+#define PPG_GSORT_END(s) (void)hipFreeAsync(gsort, s)
+
 // ------------------------------------------------------------------------------------------
 // Host-side launcher (called from ppg_api.cpp).  ring_bits selects the history ring.
 // ------------------------------------------------------------------------------------------
-// (ring bits, litlen root bits) variants; default (11, 9)
+// (ring bits, litlen root bits) variants; default (11, 8)
 #define PPG_VARIANTS(X) X(10, 8) X(10, 9) X(11, 9) X(11, 8) X(12, 9) X(12, 8) X(13, 9) X(15, 9)
 
 #ifdef PPG_STAMPS
@@ -1287,14 +1322,17 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
     if (no_census) nls = nullptr;
 #define X(R, L)                                                                                               \
     if (ring_bits == R && lit_bits == L) {                                                                    \
+        PPG_GSORT_BEGIN(s, njobs);                                                                            \
         if (nls)                                                                                              \
             hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, true>), dim3(njobs), dim3(64),                \
-                               0, s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls);                 \
+                               0, s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls, gsort);          \
         else                                                                                                  \
             hipLaunchKernelGGL((ppg_inflate_kernel<R, L, false, false>), dim3(njobs), dim3(64),               \
-                               0, s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls);                 \
+                               0, s, comp, nwords, jobs, dicts, out, res, njobs, nullptr, nls, gsort);          \
+        const hipError_t le = hipGetLastError();                                                              \
+        PPG_GSORT_END(s);                                                                                     \
         PPG_STAMP_DUMP(s);                                                                                    \
-        return hipGetLastError();                                                                             \
+        return le;                                                                                            \
     }
     PPG_VARIANTS(X)
 #undef X
@@ -1327,8 +1365,12 @@ hipError_t ppg_launch_inflate_ix(hipStream_t s, const uint32_t *comp, uint64_t n
                                  const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                  int njobs) {
     if (njobs <= 0) return hipSuccess;
+    PPG_GSORT_BEGIN(s, njobs);
     hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false>), dim3(njobs), dim3(64), 0, s, comp,
-                       nwords, jobs, dicts, out, res, njobs, blk, nullptr);
+                       nwords, jobs, dicts, out, res, njobs, blk, nullptr, gsort);
+    const hipError_t le = hipGetLastError();
+    PPG_GSORT_END(s);
+    if (le != hipSuccess) return le;
 #ifdef PPG_IX_STATS
     {
         unsigned long long h[16] = {0};
@@ -1354,9 +1396,12 @@ hipError_t ppg_launch_inflate_ixf(hipStream_t s, const uint32_t *comp, uint64_t 
                                   const uint8_t *dicts, uint8_t *out, PpgInflateResult *res, PpgBlockEnd *blk,
                                   int njobs) {
     if (njobs <= 0) return hipSuccess;
+    PPG_GSORT_BEGIN(s, njobs);
     hipLaunchKernelGGL((ppg_inflate_kernel<10, 8, true, false, true>), dim3(njobs), dim3(64), 0, s, comp, nwords, jobs,
-                       dicts, out, res, njobs, blk, nullptr);
-    return hipGetLastError();
+                       dicts, out, res, njobs, blk, nullptr, gsort);
+    const hipError_t le = hipGetLastError();
+    PPG_GSORT_END(s);
+    return le;
 }
 
 // A piece whose pass-1 symbols and exact starting history are known is written out without a second
