@@ -99,29 +99,96 @@ def shared_tiled(args, key, build, need):
     args.share_note = note
     d = os.path.join(base, "ppg_bench_" + hashlib.sha1(repr((nonce, key)).encode()).hexdigest()[:12])
     args.shm_paths.append(d)
+    failed = os.path.join(d, "failed")
     if args.local_rank == 0:
-        tf = build()
-        tf.save(d)
+        try:
+            if setup_fault("input", args.rank):
+                raise RuntimeError("injected input failure (PPG_BENCH_FAIL)")
+            tf = build()
+            tf.save(d)
+        except Exception as e:
+            # the other local ranks wait for "ready": tell them instead (they would wait 30 min)
+            try:
+                os.makedirs(d, exist_ok=True)
+                with open(failed, "w") as f:
+                    f.write(f"{type(e).__name__}: {e}")
+            except OSError:
+                pass
+            raise
         return tf, time.time() - t, f"built (shared via {d})"
     ready = os.path.join(d, "ready")
     while not os.path.exists(ready):
+        if os.path.exists(failed):
+            with open(failed) as f:
+                raise RuntimeError(f"local rank 0 failed to build the input: {f.read()}")
         if time.time() - t > 1800:
             raise TimeoutError(f"local rank 0 did not publish {d}")
         time.sleep(0.2)
     return TiledFile.load(d), time.time() - t, f"memory-mapped from {d}"
 
 
-def gather_pairs(x, y, dist_on, xdev):
-    """[(x, y) of rank 0, (x, y) of rank 1, ...] -- one all_gather (flat output: gloo wants it)."""
+def gather_vec(vals, dist_on, xdev):
+    """[vals of rank 0, vals of rank 1, ...] (floats) -- one all_gather (flat output: gloo wants it)."""
     import torch
-    v = torch.tensor([x, y], dtype=torch.float64, device=xdev)
+    v = torch.tensor([float(x) for x in vals], dtype=torch.float64, device=xdev)
     if not dist_on:
         return [v.tolist()]
     import torch.distributed as dist
     world = dist.get_world_size()
-    out = torch.zeros(world * 2, dtype=torch.float64, device=xdev)
+    out = torch.zeros(world * v.numel(), dtype=torch.float64, device=xdev)
     dist.all_gather_into_tensor(out, v)
-    return out.view(world, 2).cpu().tolist()
+    return out.view(world, v.numel()).cpu().tolist()
+
+
+def gather_pairs(x, y, dist_on, xdev):
+    """[(x, y) of rank 0, (x, y) of rank 1, ...]."""
+    return gather_vec([x, y], dist_on, xdev)
+
+
+class SetupFailed(RuntimeError):
+    """A rank's setup failed; every rank raises this with the failing ranks' messages (agree_setup)."""
+
+
+MSG_BYTES = 480
+
+
+def agree_setup(stage, err, dist_on, xdev):
+    """Setup status agreed across ranks before the next collective:
+    each rank's error (or None) from `stage` -- the input member, its shard (compressed range resident,
+    Shard, set_split), the communicator -- is all-gathered as a status + a fixed-size message, and if
+    any rank failed EVERY rank raises SetupFailed naming the failing ranks and the first one's message.
+    Without it a rank that failed setup left its peers inside the next collective: gloo's TCP teardown
+    ended the full-size world-8 rehearsal with "Connection closed by peer" on the surviving ranks
+    (gpurun_out/r05zzh/w8.log), and under RCCL they would wait until torchrun's agent killed them.
+    The reference's fan-out has no such step (BatchedFASTQ.cs:62-77: one process, Task.Run per chunk)."""
+    if not dist_on:
+        if err is not None:
+            raise err
+        return
+    import torch
+    import torch.distributed as dist
+    msg = b"" if err is None else f"{type(err).__name__}: {err}".encode(errors="replace")[:MSG_BYTES - 1]
+    v = torch.zeros(MSG_BYTES, dtype=torch.uint8)
+    v[0] = 0 if err is None else 1
+    if msg:
+        v[1:1 + len(msg)] = torch.frombuffer(bytearray(msg), dtype=torch.uint8)
+    world = dist.get_world_size()
+    out = torch.zeros(world * MSG_BYTES, dtype=torch.uint8, device=xdev)
+    dist.all_gather_into_tensor(out, v.to(xdev))
+    rows = out.view(world, MSG_BYTES).cpu().numpy()
+    bad = [r for r in range(world) if rows[r, 0]]
+    if not bad:
+        return
+    first = bytes(rows[bad[0], 1:]).rstrip(b"\0").decode(errors="replace")
+    raise SetupFailed(f"setup failed at '{stage}' on rank(s) {bad} of {world}; rank {bad[0]}: {first}")
+
+
+def setup_fault(stage, rank):
+    """Test hook (tests only, never set by the driver): PPG_BENCH_FAIL="<stage>@<rank>" makes that
+    rank's setup fail at that stage -- input, shard, set_split (a real library error: side points
+    outside their chunks) or comm."""
+    v = os.environ.get("PPG_BENCH_FAIL", "")
+    return bool(v) and v == f"{stage}@{rank}"
 
 
 def drop_shared(args):
@@ -349,6 +416,99 @@ def ingest_run(tf, ix, dev, threads, piece_gib=8.0, enum_gib=0.0):
         return out, enum
     finally:
         if os.path.exists(path):
+            os.remove(path)
+
+
+def ingest_pieces(args, tf, a, b, slots):
+    """(piece_bytes, waves per chunk) for a rank's end-to-end leg over chunks [a, b): about four
+    pieces per rank (<= --ingest-piece-gib), so the read of piece k+1 overlaps the decode of piece k
+    even for an N = 8 rank's ~6 GB; chunks split at side points (<= 16 waves) into enough waves for
+    ~1.5 generations per piece, as the resident split does for a small rank."""
+    rng = int(tf.p_input[b] - tf.p_input[a]) + 1
+    pb = int(min(args.ingest_piece_gib * (1 << 30), max(1 << 30, rng / 4)))
+    per_piece = max(1, (b - a) * pb // max(1, rng))
+    return pb, int(min(16, max(1, -(-3 * slots // (2 * per_piece)))))
+
+
+def dist_ingest_run(tf, args, ctx, a, b, rank, world, dist_on, xdev):
+    """The N > 1 end-to-end leg (and a --share rehearsal's): local rank 0 writes the member to a
+    file once (the directory with room for it: share_dir), every rank streams its own chunk range
+    [a, b) from it -- pread into pinned buffers, H2D, decode, piece by piece (ppg_file_decompress_all,
+    the role of LazyFileReader.cs:41-97 feeding BatchedFASTQ.cs:62-77's tasks) -- one untimed run, a
+    barrier, the timed run; the per-rank seconds and record totals are gathered and the records
+    checked exactly.  Every decision and failure is agreed across ranks, so no rank is left in a
+    collective.  Never the bench value."""
+    import torch
+    import parallelparsing_amd as pp
+    pick = [None, None]
+    if rank == 0:
+        try:
+            base, note = share_dir(os.environ.get("TMPDIR") or "/tmp", tf.file_len)
+            pick = [os.path.join(base, f"ppg_e2e_{os.getpid()}_{int(time.time())}.fastq.gz"), note]
+        except OSError as e:
+            pick = [None, str(e)]
+    if dist_on:
+        import torch.distributed as dist
+        dist.broadcast_object_list(pick, 0)
+    path, note = pick
+    if path is None:
+        return {"error": f"no room for the {tf.file_len / 1e9:.1f} GB file: {note}"}
+    err, wt = None, 0.0
+    if args.local_rank == 0:
+        try:
+            t = time.perf_counter()
+            with open(path, "wb") as f:
+                for lo in range(0, tf.file_len, 1 << 30):
+                    f.write(tf.file_bytes(lo, min(tf.file_len, lo + (1 << 30))))
+            wt = time.perf_counter() - t
+        except OSError as e:
+            err = e
+    try:
+        try:
+            agree_setup("e2e file", err, dist_on, xdev)
+        except (SetupFailed, OSError) as e:
+            return {"error": str(e)}
+        pb, waves = ingest_pieces(args, tf, a, b, wave_slots(torch.device("cuda", ctx.device)))
+        status, sec, recs = 0.0, 0.0, 0
+        try:
+            ix = tf.index(a, b + 1)
+            if waves > 1:
+                ix.set_side_points(*tf.side_points(a, b + 1, waves))
+            pp.decompress_file(ix, path, 0, b - a, piece_bytes=pb, threads=args.host_threads, device=ctx)  # warm
+            if dist_on:
+                dist.barrier()
+            _, recs, sec = pp.decompress_file(ix, path, 0, b - a, piece_bytes=pb, threads=args.host_threads,
+                                              device=ctx)
+        except (pp.PpgError, OSError, RuntimeError) as e:
+            status = 1.0
+            log(f"[bench] rank {rank}: end-to-end leg failed: {e}")
+        finally:
+            ctx.release_file_buffers()
+        rows = gather_vec([status, sec, recs, b - a, int(tf.p_input[b] - tf.p_input[a]) + 1], dist_on, xdev)
+        if any(r[0] for r in rows):
+            return {"error": f"ppg_file_decompress_all failed on rank(s) {[i for i, r in enumerate(rows) if r[0]]}"}
+        total = int(sum(r[2] for r in rows))
+        smax = max(r[1] for r in rows)
+        exact = args.share > 1 or total == tf.expected_records()
+        assert exact, ("end-to-end records", total, tf.expected_records())
+        gz = sum(r[4] for r in rows)
+        return {"records_per_s": total / smax, "compressed_GBps": gz / smax / 1e9,
+                "decompressed_GBps": (tf.text_len * tf.repeats if args.share == 1 else
+                                      int(tf.p_output[b] - tf.p_output[a])) / smax / 1e9,
+                "seconds_max_over_ranks": smax, "records": total,
+                "per_rank": [{"rank": i, "seconds": round(r[1], 4), "records": int(r[2]), "chunks": int(r[3]),
+                              "gz_GB": round(r[4] / 1e9, 3), "compressed_GBps": round(r[4] / max(r[1], 1e-9) / 1e9, 2)}
+                             for i, r in enumerate(rows)],
+                "piece_GiB": round(pb / (1 << 30), 3), "waves_per_chunk": f"<= {waves} (side points)",
+                "file_GB": tf.file_len / 1e9, "write_s": wt, **({"dir_note": note} if note else {}),
+                "note": "every rank: its chunk range of the file (page cache) -> pread -> pinned -> H2D -> decode, "
+                        "piece by piece (ppg_file_decompress_all, three device slots); one untimed run, a barrier, "
+                        "then the timed run; records exact over all ranks; PCIe-inclusive, not the bench value"
+                        + ("; --share rehearsal: rank 0's range alone" if args.share > 1 else "")}
+    finally:
+        if dist_on:
+            dist.barrier()
+        if args.local_rank == 0 and os.path.exists(path):
             os.remove(path)
 
 
@@ -948,7 +1108,7 @@ def main():
         args.scaling = "strong" if world > 1 else "weak"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    args.local_rank, args.shm_paths = local, []
+    args.local_rank, args.rank, args.shm_paths = local, rank, []
     # PPG_BENCH_FORCE_DIST=1 (tests): the N > 1 glue -- process group, the library's RCCL
     # communicator from a broadcast unique id, the count all-gather -- even at world size 1
     dist_on = world > 1 or os.environ.get("PPG_BENCH_FORCE_DIST") == "1"
@@ -989,7 +1149,35 @@ def main():
             dist.destroy_process_group()
         return
 
-    tf = build_input(args)
+    try:
+        return run_bench(args, dev, world, rank, local, dist_on, backend, xdev)
+    except SetupFailed as e:
+        # every rank got here with the same message (agree_setup): exit non-zero, no rank stranded
+        log(f"[bench] rank {rank}: {e}")
+        drop_shared(args)   # every rank is past the agreement: the shared input (or its failure file) can go
+        if dist_on:
+            dist.destroy_process_group()
+        sys.exit(3)
+
+
+def run_bench(args, dev, world, rank, local, dist_on, backend, xdev):
+    import torch
+    import parallelparsing_amd as pp
+    from parallelparsing_amd.dist import partition_chunks, gather_counts
+    if dist_on:
+        import torch.distributed as dist
+
+    # setup, in stages whose status every rank agrees on before the next collective (agree_setup)
+    err = tf = None
+    try:
+        if setup_fault("input", rank) and local != 0:
+            raise RuntimeError("injected input failure (PPG_BENCH_FAIL)")
+        tf = build_input(args)
+    except SetupFailed:
+        raise
+    except Exception as e:   # noqa: BLE001 - agreed with the other ranks, then raised on all of them
+        err = e
+    agree_setup("input", err, dist_on, xdev)
     ix_out, ix_in = tf.p_output, tf.p_input
     nchunks = tf.npoints - 1
     ranges = partition_chunks(ix_in, world)
@@ -1000,30 +1188,49 @@ def main():
         ranges = [(a, b)]
     lo, hi = int(ix_in[a]) - 1, int(ix_in[b])   # file bytes [Input_a - 1, Input_b - 1]
     comp_len = hi - lo
-    t = time.time()
     t_setup = time.time()
-    comp = torch.empty(comp_len + 256, dtype=torch.uint8, device=dev)
-    comp[comp_len:].zero_()
-    tf.fill_device(comp, lo, hi)
-    torch.cuda.synchronize()
-    index = tf.index(a, b + 1)   # this rank's points only: its chunks are index chunks 0..b-a-1
-    ctx = pp.Device(local)
-    out_cap = int(args.out_capacity_gib * (1 << 30))
-    shard = pp.Shard(index, comp.data_ptr(), first=0, n=b - a, device=ctx, comp_on_device=True, comp_len=comp_len,
-                     out_capacity=out_cap)
-    args.split, ksplit = auto_split(args, wave_slots(dev), b - a)
-    if args.split > 1:
-        sb, so, sw = split_points(tf, args, b - ksplit, b, wave_slots(dev))
-        shard.set_split(sb, so, sw)
-        log(f"[bench] rank {rank}: last {ksplit} chunks split, {b - a + sb.size} waves ({sb.size} side points)")
-    args.split_chunks = ksplit if args.split > 1 else 0
-    args.tail2_s, args.tail2_k = tail2_split(args, wave_slots(dev), ksplit) if args.split > 1 else (1, 0)
-    n_side = int(sb.size) if args.split > 1 else 0
+    err = comp = shard = ctx = None
+    n_side = 0
+    try:
+        if setup_fault("shard", rank):
+            raise RuntimeError("injected shard failure (PPG_BENCH_FAIL)")
+        comp = torch.empty(comp_len + 256, dtype=torch.uint8, device=dev)
+        comp[comp_len:].zero_()
+        tf.fill_device(comp, lo, hi)
+        torch.cuda.synchronize()
+        index = tf.index(a, b + 1)   # this rank's points only: its chunks are index chunks 0..b-a-1
+        ctx = pp.Device(local)
+        out_cap = int(args.out_capacity_gib * (1 << 30))
+        shard = pp.Shard(index, comp.data_ptr(), first=0, n=b - a, device=ctx, comp_on_device=True,
+                         comp_len=comp_len, out_capacity=out_cap)
+        args.split, ksplit = auto_split(args, wave_slots(dev), b - a)
+        if args.split > 1:
+            sb, so, sw = split_points(tf, args, b - ksplit, b, wave_slots(dev))
+            if setup_fault("set_split", rank):
+                # a real library error: side points past their chunks' outputs (PPG_ARG_ERROR)
+                so = so + int(ix_out[b] - ix_out[a]) + (1 << 20)
+            shard.set_split(sb, so, sw)
+            n_side = int(sb.size)
+            log(f"[bench] rank {rank}: last {ksplit} chunks split, {b - a + sb.size} waves ({sb.size} side points)")
+        args.split_chunks = ksplit if args.split > 1 else 0
+        args.tail2_s, args.tail2_k = tail2_split(args, wave_slots(dev), ksplit) if args.split > 1 else (1, 0)
+    except Exception as e:   # noqa: BLE001 - agreed with the other ranks, then raised on all of them
+        err = e
+    agree_setup("shard", err, dist_on, xdev)
     setup_s = time.time() - t_setup
     log(f"[bench] rank {rank}: chunks [{a},{b}) {comp_len / 1e9:.2f} GB gz resident, "
         f"{shard.batches} output batch(es), setup {setup_s:.1f}s")
     counts_dev = torch.zeros(max(1, b - a), dtype=torch.int64, device=dev)
-    comm, gather_via = (None, None) if not dist_on else make_comm(ctx, world, rank, backend, xdev)
+    err = None
+    comm, gather_via = None, None
+    try:
+        if setup_fault("comm", rank):
+            raise RuntimeError("injected communicator failure (PPG_BENCH_FAIL)")
+        if dist_on:
+            comm, gather_via = make_comm(ctx, world, rank, backend, xdev)
+    except Exception as e:   # noqa: BLE001 - agreed with the other ranks, then raised on all of them
+        err = e
+    agree_setup("comm", err, dist_on, xdev)
     bounds = np.array([r[0] for r in ranges] + [ranges[-1][1]], np.int32)
     # per-rank setup seconds (input ready, shard ready) of every rank, in the line
     setup_ranks = gather_pairs(args.input_seconds, setup_s, dist_on, xdev)
@@ -1068,6 +1275,7 @@ def main():
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    own_elapsed = elapsed
     if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -1075,6 +1283,14 @@ def main():
 
     # correctness of the run (size-independent checks; bit parity is tests/test_gpu_parity.py)
     r = shard.results()
+    # per-rank evidence: every rank's own step time, inflate launch time,
+    # output batches, chunks, waves and records, so an N > 1 curve can be diagnosed from its line
+    per_rank = [{"rank": i, "ms_per_step": round(v[0], 3), "inflate_ms_per_step": round(v[1], 3),
+                 "parse_ms_per_step": round(v[2], 3), "batches": int(v[3]), "chunks": int(v[4]),
+                 "waves": int(v[5]), "records": int(v[6]), "gz_GB": round(v[7] / 1e9, 3)}
+                for i, v in enumerate(gather_vec([own_elapsed / args.steps * 1e3, infl_ms / args.steps,
+                                                  parse_ms / args.steps, shard.batches, b - a, b - a + n_side,
+                                                  int(r["records"].sum()), comp_len], dist_on, xdev))]
     assert (r["status"] == 0).all(), "chunk errors"
     assert (r["produced"] == (ix_out[a + 1:b + 1] - ix_out[a:b])).all(), "produced != to.Output - from.Output"
     local_records = int(r["records"].sum())
@@ -1152,12 +1368,27 @@ def main():
         "setup_s": {"input_how": args.input_how, **({"share_dir_note": args.share_note} if getattr(args, "share_note", None) else {}),
                     "per_rank": [{"input": round(x, 2), "shard": round(y, 2)}
                                                                for x, y in setup_ranks]},
+        "per_rank": {"ranks": per_rank,
+                     "ms_per_step_min_max": [min(p["ms_per_step"] for p in per_rank),
+                                             max(p["ms_per_step"] for p in per_rank)],
+                     "inflate_ms_min_max": [min(p["inflate_ms_per_step"] for p in per_rank),
+                                            max(p["inflate_ms_per_step"] for p in per_rank)],
+                     "note": "each rank's own clock over the timed steps (value uses the max over ranks, "
+                             "barrier-bracketed); inflate/parse: HIP-event launch times of its shard"},
     }
+    if (dist_on or args.share > 1) and args.workload == "50gb" and not args.no_ingest and not args.blank_lines:
+        # end to end at N > 1 ("scaling limits are host file read and
+        # PCIe H2D"): every rank streams its own [P[a].Input - 1, P[b].Input - 1] range of the member
+        # from a file in page cache (LazyFileReader.cs:41-97's role) through ppg_file_decompress_all;
+        # max-over-ranks seconds beside the resident number.  The resident shard is freed first.
+        shard = comp = None
+        torch.cuda.empty_cache()
+        line["ingest"] = dist_ingest_run(tf, args, ctx, a, b, rank, world, dist_on, xdev)
     args.ingest = world == 1 and args.workload == "50gb" and not args.no_ingest and not args.blank_lines and args.share == 1
     chunk_legs = world == 1 and args.workload == "50gb" and not args.no_chunk_api and args.share == 1
     if rank == 0 and world == 1 and (args.ingest or args.create_index or chunk_legs):
         # the measured shard (~270 GB of HBM at configs[2]) is done with: the legs below get the device
-        del shard, comp
+        shard = comp = None
         torch.cuda.empty_cache()
         # (r05: allocations over the freed HBM are slow for seconds after -- one of 284 GB right
         # after took 7.9 s, the first multi-GB grow of a launch slot's scratch 3.3-5.6 s; the

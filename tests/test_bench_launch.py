@@ -107,3 +107,99 @@ def test_share_dir_falls_back_when_shm_is_small(monkeypatch, tmp_path):
         raise AssertionError("no room anywhere must raise")
     except OSError as e:
         assert "GiB free" in str(e)
+
+
+def _agree_rank(rank, world, port, bad, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import bench
+    out = []
+    for stage in ("input", "shard", "comm"):
+        err = RuntimeError(f"rank {rank} broke at {stage}") if (rank, stage) in bad else None
+        try:
+            bench.agree_setup(stage, err, True, "cpu")
+            out.append((stage, "ok"))
+        except bench.SetupFailed as e:
+            out.append((stage, str(e)))
+            break
+    # a collective after the agreement still meets (nobody is stranded)
+    dist.barrier()
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def _agree(world, bad):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_agree_rank, args=(r, world, port, bad, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    return got
+
+
+def test_setup_failure_on_one_rank_is_every_ranks_failure():
+    """a setup stage that fails on rank 1 (gloo, world 2) makes BOTH ranks raise
+    SetupFailed at that stage with rank 1's message -- no rank goes on into the next collective."""
+    got = _agree(2, {(1, "shard")})
+    for r in (0, 1):
+        assert got[r][0] == ("input", "ok")
+        stage, msg = got[r][1]
+        assert stage == "shard" and "on rank(s) [1] of 2" in msg and "rank 1 broke at shard" in msg
+        assert len(got[r]) == 2
+
+
+def test_setup_failure_names_every_failing_rank():
+    got = _agree(4, {(2, "comm"), (3, "comm")})
+    for r in range(4):
+        assert [s for s, _ in got[r]] == ["input", "shard", "comm"]
+        msg = got[r][2][1]
+        assert "on rank(s) [2, 3] of 4" in msg and "rank 2 broke at comm" in msg
+
+
+def test_setup_agreement_single_process_raises_its_own_error():
+    sys.path.insert(0, ROOT)
+    import bench
+    bench.agree_setup("shard", None, False, "cpu")
+    try:
+        bench.agree_setup("shard", ValueError("x"), False, "cpu")
+        raise AssertionError("must raise")
+    except ValueError:
+        pass
+    os.environ["PPG_BENCH_FAIL"] = "set_split@3"
+    try:
+        assert bench.setup_fault("set_split", 3) and not bench.setup_fault("set_split", 2)
+        assert not bench.setup_fault("shard", 3)
+    finally:
+        del os.environ["PPG_BENCH_FAIL"]
+
+
+def test_ingest_pieces_keep_four_pieces_per_rank():
+    """The N > 1 end-to-end leg's piece size and split (bench.ingest_pieces) on configs[3]'s shape."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import numpy as np
+
+    class TF:   # ~50 GB over 52,467 chunks, as the default member
+        p_input = np.linspace(11, 50e9, 52468).astype(np.int64)
+
+    class A:
+        ingest_piece_gib = 8.0
+    slots = 256 * 32
+    for world in (2, 4, 8):
+        a, b = 0, 52467 // world
+        pb, waves = bench.ingest_pieces(A, TF, a, b, slots)
+        rng = TF.p_input[b] - TF.p_input[a] + 1
+        assert 3.9 <= rng / pb <= 4.1 or pb == 8 << 30
+        assert 1 <= waves <= 16
+    assert bench.ingest_pieces(A, TF, 0, 52467 // 8, slots)[1] > bench.ingest_pieces(A, TF, 0, 52467 // 2, slots)[1]

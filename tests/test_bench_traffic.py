@@ -54,3 +54,22 @@ def test_issue_roofline_only_for_the_same_build(tmp_path):
     assert abs(r["salu_per_cu_cycle"] - 0.5) < 1e-9 and abs(r["valu_busy"] - 0.5) < 1e-9
     assert bench.issue_roofline({"ppg_version": "v", "build_id": "inflate-bbbb"}, str(p)) is None
     assert bench.issue_roofline(b, str(tmp_path / "missing.json")) is None
+
+
+def test_committed_stall_and_traffic_files_name_the_same_kernel():
+    """roofline.issue's source (profiles/inflate_stalls.json) and roofline.traffic's
+    (profiles/traffic.json) must describe the same inflate instantiation and build; the stall file's
+    label comes from the rocprof rows it sums (tools/stall_summary.py), never a literal."""
+    with open(os.path.join(ROOT, "profiles", "inflate_stalls.json")) as f:
+        st = json.load(f)
+    with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+        tr = json.load(f)
+    assert st["kernel"] == tr["kernel"], (st["kernel"], tr["kernel"])
+    assert st["build"] == tr["build"]
+
+
+def test_stall_label_comes_from_the_rows():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import stall_summary
+    n = "void ppg_inflate_kernel<11, 8, false, true, false>(unsigned int const*, unsigned long, PpgInflateJob const*)"
+    assert stall_summary.kernel_label(n) == "ppg_inflate_kernel<11, 8, false, true, false>"

@@ -13,15 +13,19 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(args, ranks=1, timeout=240):
-    env = dict(os.environ, PPG_BENCH_ONE_DEVICE="1", PPG_DIST_BACKEND="gloo")
+def _bench_raw(args, ranks=1, timeout=240, env_extra=None):
+    env = dict(os.environ, PPG_BENCH_ONE_DEVICE="1", PPG_DIST_BACKEND="gloo", **(env_extra or {}))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
     if ranks > 1 and "--gpus" not in args:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
                "--master-addr", "127.0.0.1", "--master-port", str(29400 + os.getpid() % 500)] + cmd[1:]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _bench(args, ranks=1, timeout=240):
+    r = _bench_raw(args, ranks, timeout)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -96,3 +100,43 @@ def test_bench_world8_rehearsal():
     assert eight["communicator"]["world_size"] == 8
     assert "ppg_shard_gather_counts" in eight["communicator"]["count_gather"]
     assert len(eight["setup_s"]["per_rank"]) == 8
+
+
+@pytest.mark.parametrize("world,fail", [(2, "set_split@1"), (8, "shard@5"), (8, "input@0")])
+def test_setup_failure_fails_every_rank_loudly(world, fail):
+    """one rank's setup failure -- a real library error from ppg_shard_set_split
+    (side points past their chunks), or an injected one at the shard / input stage (local rank 0's
+    build: the waiting ranks read its failure file) -- is agreed before the next collective: every
+    rank exits non-zero naming the failing rank, promptly, instead of stranding its peers in gloo /
+    RCCL (PPG_BENCH_FAIL, a test hook)."""
+    import time
+    stage, bad = fail.split("@")
+    t = time.time()
+    r = _bench_raw(SMALL + ["--gpus", str(world)], timeout=300, env_extra={"PPG_BENCH_FAIL": fail})
+    assert r.returncode != 0, r.stdout[-2000:]
+    agreed = "shard" if stage == "set_split" else stage
+    # input@0: local rank 0 could not build the member, so every rank lacks its input
+    want = (f"setup failed at 'input' on rank(s) {list(range(world))} of {world}; rank 0: RuntimeError: injected"
+            if fail == "input@0" else f"setup failed at '{agreed}' on rank(s) [{bad}] of {world}")
+    lines = [ln for ln in r.stderr.splitlines() if want in ln]
+    assert len({ln.split(":")[0] for ln in lines}) == world, r.stderr[-3000:]   # every rank said so
+    if stage == "set_split":
+        assert "ppg_shard_set_split" in r.stderr or "ARG_ERROR" in r.stderr or "PpgError" in r.stderr, r.stderr[-3000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert time.time() - t < 240
+
+
+def test_bench_world8_rehearsal_end_to_end_leg():
+    """The N > 1 line's per-rank evidence and end-to-end leg, world 8 on the one
+    GPU: every rank's own step / inflate times, batches and records; every rank streams its range of
+    the member from a file through ppg_file_decompress_all, max-over-ranks seconds, records exact."""
+    args = [a for a in SMALL if a != "--no-ingest"] + ["--repeats", "16", "--gpus", "8", "--ingest-piece-gib", "0.25"]
+    eight = _bench(args, timeout=420)
+    pr = eight["per_rank"]["ranks"]
+    assert [p["rank"] for p in pr] == list(range(8))
+    assert sum(p["records"] for p in pr) == eight["config"]["records"]
+    assert all(p["batches"] >= 1 and p["inflate_ms_per_step"] > 0 for p in pr)
+    ing = eight["ingest"]
+    assert "error" not in ing, ing
+    assert ing["records"] == eight["config"]["records"] and len(ing["per_rank"]) == 8
+    assert ing["seconds_max_over_ranks"] == max(p["seconds"] for p in ing["per_rank"])

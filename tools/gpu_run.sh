@@ -86,6 +86,13 @@ run_step() {
       timeout -k 10 300 python3 -u bench.py --steps ${STEPS:-5} --warmup 2 $NOLEGS ${a//_/ } > $O/shares/v_${spec%%:*}.json 2> $O/shares/v_${spec%%:*}.log || return $?
       line $O/shares/v_${spec%%:*}.json
     done ;;
+  e2eshares)   # rank 0's share of an N-way split, resident AND end to end from a file (r06)
+    mkdir -p $O/shares
+    for n in ${SHARES-2 4 8}; do
+      timeout -k 10 400 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --share $n $xa > $O/shares/e2e$n.json 2> $O/shares/e2e$n.log || return $?
+      line $O/shares/e2e$n.json
+      python3 -c "import json,sys; d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1]; i=d.get('ingest',{}); print({k: i.get(k) for k in ('records_per_s','compressed_GBps','seconds_max_over_ranks','piece_GiB','waves_per_chunk','error')})" $O/shares/e2e$n.json
+    done ;;
   ab)
     timeout -k 10 900 python3 -u tools/ab_multi.py $AB_ARGS $AB_BUILDS > $O/ab.json 2> $O/ab.log || { tail -5 $O/ab.log; return 1; }
     tail -c 1500 $O/ab.json ;;

@@ -21,23 +21,34 @@ G = os.path.join(ROOT, "gpurun_out")
 
 def passes():
     """Counter totals over the inflate launches; a counter collected in several passes is taken from
-    the first pass that has it (not summed over passes)."""
-    out = {}
+    the first pass that has it (not summed over passes).  Also returns the kernel instantiation(s)
+    the summed rows name (VERDICT r05 next #3: the label comes from the rows, not a literal)."""
+    out, names = {}, set()
     for path in sorted(glob.glob(os.path.join(G, "stall_*", "**", "*counter_collection.csv"), recursive=True)):
         tot = defaultdict(float)
         for r in csv.DictReader(open(path)):
             if "ppg_inflate_kernel" in r["Kernel_Name"]:
                 tot[r["Counter_Name"]] += float(r["Counter_Value"])
+                names.add(kernel_label(r["Kernel_Name"]))
         for k, v in tot.items():
             out.setdefault(k, v)
-    return out
+    return out, sorted(names)
+
+
+def kernel_label(name):
+    """'void ppg_inflate_kernel<11, 8, false, true, false>(unsigned int const*, ...)' ->
+    'ppg_inflate_kernel<11, 8, false, true, false>' (the form traffic.json's "kernel" uses)."""
+    m = re.search(r"ppg_inflate_kernel<[^>]*>", name)
+    return m.group(0) if m else name
 
 
 def main(tag):
-    c = passes()
+    c, names = passes()
+    if len(names) != 1:
+        raise SystemExit(f"the stall passes summed over {len(names)} inflate instantiations: {names}")
     wc = c["SQ_WAVE_CYCLES"]
     out = {
-        "kernel": "ppg_inflate_kernel<10, 8, false, true, false>",
+        "kernel": names[0],
         "workload": "bench.py --repeats 40 --steps 1 (40 x 4.04 GB text, chunk = 10,000), one launch",
         "command": "tools/pmc_stalls.sh: one rocprofv3 --pmc pass per counter group (A-E)",
         "counters": c,
