@@ -39,7 +39,8 @@ REFERENCE_REC_S = 1.217e6  # Plots/csv_original/parallel_10k_false.csv:8 (Arm64,
 
 
 def log(*a):
-    print(*a, file=sys.stderr, flush=True)
+    sys.stderr.write(" ".join(map(str, a)) + "\n")   # one write: ranks' lines do not interleave mid-line
+    sys.stderr.flush()
 
 
 def free_bytes(path):
@@ -336,9 +337,10 @@ def issue_roofline(build, path=None):
             "workload": t.get("workload")}
 
 
-def pcie_d2h_GBps(dev, gib=4):
+def pcie_d2h_GBps(dev, gib=4, h2d=False):
     """Device -> pinned host copy rate of this box (the bound of any leg that lands decompressed
-    text in host memory): one 4 GiB hipMemcpy, best of three."""
+    text in host memory), or with h2d pinned host -> device (the bound of the ingest leg, whose
+    compressed bytes cross that way): one 4 GiB hipMemcpy, best of three."""
     import torch
     n = gib << 30
     d = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -347,7 +349,10 @@ def pcie_d2h_GBps(dev, gib=4):
     for _ in range(3):
         torch.cuda.synchronize()
         t = time.perf_counter()
-        h.copy_(d, non_blocking=True)
+        if h2d:
+            d.copy_(h, non_blocking=True)
+        else:
+            h.copy_(d, non_blocking=True)
         torch.cuda.synchronize()
         best = max(best, n / (time.perf_counter() - t) / 1e9)
     del d, h
@@ -399,7 +404,10 @@ def ingest_run(tf, ix, dev, threads, piece_gib=8.0, enum_gib=0.0):
         pp.decompress_file(ix, path, device=dev, threads=threads, piece_bytes=pb)   # warm: buffers, page cache
         _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=threads, piece_bytes=pb)
         assert tot == tf.expected_records(), (tot, tf.expected_records())
+        import torch
+        h2d = pcie_d2h_GBps(torch.device("cuda", dev.device), h2d=True)
         out = {"records_per_s": tot / sec, "compressed_GBps": tf.file_len / sec / 1e9,
+               "pcie_h2d_GBps": h2d, "frac_of_pcie_bound": tf.file_len / sec / 1e9 / h2d,
                "decompressed_GBps": tf.text_len * tf.repeats / sec / 1e9, "seconds": sec,
                "file_GB": tf.file_len / 1e9, "write_s": wt,
                "note": f"file in page cache -> pread ({threads} threads) -> pinned -> H2D -> decode, {piece_gib:g} GiB "
@@ -1156,6 +1164,8 @@ def main():
         log(f"[bench] rank {rank}: {e}")
         drop_shared(args)   # every rank is past the agreement: the shared input (or its failure file) can go
         if dist_on:
+            # every rank has said so before any exits (torchrun stops the others at the first exit)
+            dist.barrier()
             dist.destroy_process_group()
         sys.exit(3)
 

@@ -405,6 +405,10 @@ void ppg_pairs_free(ppg_pairs *p);
  *      PPG_STREAM_END when there is none.  N ranks: the first call is collective (every rank calls
  *      it: the records a rank does not hold move from their ranks over ppg_comm_alltoallv -- RCCL
  *      ncclSend / ncclRecv over xGMI, or the host transport) and is the rank's one window.
+ *      A half's descriptors are 32-bit positions, so a half of 4 GiB or more (pair_chunk of ~11 M
+ *      150 bp records) is PPG_UNSUPPORTED, before anything of it is packed (N ranks: agreed in the
+ *      exchange's status gather, or after the exchange).  PPG_DATA_ERROR if the shards' batches cannot
+ *      complete a pair chunk (never expected: the emission ends instead of looping).
  *  ppg_pairs_chunk       device pointers of a half of the current window (valid until the next call).
  *  ppg_pairs_copy_chunk  a half into caller memory (bytes and/or descriptors; NULL skips).
  *  ppg_pairs_emit_stats  [0] ms (re-)running batches, [1] ms packing, [2] ms exchanging, [3] ms in

@@ -1202,10 +1202,19 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             int64_t off, len;
             range(k, off, len);
             uint8_t *dst = S.db[k % kPieces].p;
+            double wait_ms = 0, read_ms = 0, slow_ms = 0;   // (PPG_INGEST_VERBOSE) slot waits, preads, slowest pread
             for (int64_t r = 0; r < len && rcp == PPG_OK; r += kSlotBytes, slot = (slot + 1) % kSlots) {
                 const int64_t m = std::min(kSlotBytes, len - r);
+                const double tw = verbose ? now_ms() : 0;
                 if (hipEventSynchronize(S.slot_ev[slot]) != hipSuccess) { rcp = PPG_DEVICE_ERROR; break; }
+                const double tr = verbose ? now_ms() : 0;
                 if (!pread_parallel(fd, S.slot[slot].p, off + r, m, threads)) { rcp = PPG_IO_ERROR; break; }
+                if (verbose) {
+                    const double te = now_ms();
+                    wait_ms += tr - tw;
+                    read_ms += te - tr;
+                    slow_ms = std::max(slow_ms, te - tr);
+                }
                 if (hipMemcpyAsync(dst + r, S.slot[slot].p, (size_t)m, hipMemcpyHostToDevice, S.cs) != hipSuccess ||
                     hipEventRecord(S.slot_ev[slot], S.cs) != hipSuccess)
                     rcp = PPG_DEVICE_ERROR;
@@ -1214,8 +1223,9 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
                                   hipEventRecord(S.piece_ev[k % kPieces], S.cs) != hipSuccess))
                 rcp = PPG_DEVICE_ERROR;
             if (verbose)
-                fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms\n", k, len / 1e6, t1,
-                        now_ms() - t1);
+                fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms (pread %.1f ms, slowest "
+                        "128 MB %.1f ms; waiting for pinned slots %.1f ms)\n", k, len / 1e6, t1, now_ms() - t1, read_ms,
+                        slow_ms, wait_ms);
             std::lock_guard<std::mutex> lk(mu);
             if (rcp != PPG_OK) prod_rc = rcp;
             else ready = k + 1;

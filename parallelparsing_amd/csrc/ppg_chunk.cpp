@@ -818,6 +818,9 @@ int find_mat(ChunkSlot &sl, const uint32_t *comp, uint64_t nwords, const uint8_t
             pmi[c][i].end_bit = i + 1 < pmi[c].size() ? (uint64_t)pbit[c][i] : last_end;
         if (pmi[c].empty()) covered[c] = 0;
     }
+    // the H2D sources above (g, sl_all, cs) are pageable vectors that die here: wait for the copies
+    // (the phase clock syncs only when verbose)
+    HIPCHK(hipStreamSynchronize(s));
     clk.mark("f.resolve", s);
     return PPG_OK;
 }
@@ -855,20 +858,31 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
         comp_len += ((size_t)r->slice_len + kSliceAlign - 1) / kSliceAlign * kSliceAlign;
     }
     if (go.empty()) return PPG_OK;
+    // the materialise path (find_mat) takes launches of plain indexes up to kMatMaxChunks
+    bool mat = go.size() <= (size_t)kMatMaxChunks && !getenv("PPG_CHUNK_NO_FIND") && !getenv("PPG_CHUNK_NO_MAT");
+    for (size_t i = 0; mat && i < go.size(); i++) mat = go[i]->ix->side_out.empty();
     {   // the shard's buffers with headroom, so launches of growing size do not reallocate each time
-        size_t n = go.size(), offb = 0, tot = 0, nsub = 0;
+        size_t n = go.size(), offb = 0, tot = 0, nsub = 0, nwin = 0;
         for (ChunkReq *r : go) {
             const PpgPoint &from = r->ix->pts[(size_t)r->k], &to = r->ix->pts[(size_t)r->k + 1];
             offb += from.offset.size();
             tot += (size_t)std::max<int64_t>(to.output - from.output, 0);
             const auto &O = r->ix->side_out;
-            nsub += (size_t)std::max<std::ptrdiff_t>(0, std::lower_bound(O.begin(), O.end(), to.output) -
-                                                            std::upper_bound(O.begin(), O.end(), from.output));
-            if (O.empty() && n <= (size_t)kFindMaxChunks) nsub += kMatRanges;   // the block search's at most
+            const size_t own = (size_t)std::max<std::ptrdiff_t>(0, std::lower_bound(O.begin(), O.end(), to.output) -
+                                                                      std::upper_bound(O.begin(), O.end(), from.output));
+            nsub += own;
+            nwin += own;
+            if (O.empty() && n <= (size_t)kFindMaxChunks) {
+                nsub += kMatRanges;   // the block search's pieces at most
+                // side windows: the materialise path fills none (its pieces start from resolved
+                // histories, not dictionaries); find_side_points at most 15 per chunk (ADVICE r05:
+                // 48 windows of 32 KiB per chunk were reserved and never written, ~400 MB per slot)
+                if (!mat) nwin += 16;
+            }
         }
         ppg_shard *sh = sl.sh;
         HIPCHK(grow_buf(sh->jobs, n));
-        HIPCHK(grow_buf(sh->dicts, (n + nsub) * kWin));
+        HIPCHK(grow_buf(sh->dicts, (n + nwin) * kWin));
         HIPCHK(grow_buf(sh->offs, offb + 16));
         HIPCHK(grow_buf(sh->oref, n));
         HIPCHK(grow_buf(sh->res, n));
@@ -901,8 +915,6 @@ int run_launch(ppg_ctx *ctx, ChunkService &svc, ChunkSlot &sl, std::vector<Chunk
     int rc = shard_prepare_specs(sh, spec.data(), (int32_t)go.size(), sl.comp.p, (int64_t)comp_len, 0, sl.s, nullptr);
     if (rc != PPG_OK) return rc;
     pc.mark("prepare");
-    bool mat = go.size() <= (size_t)kMatMaxChunks && !getenv("PPG_CHUNK_NO_FIND") && !getenv("PPG_CHUNK_NO_MAT");
-    for (size_t i = 0; mat && i < go.size(); i++) mat = go[i]->ix->side_out.empty();
     if (mat) {   // the materialise path (find_mat above)
         std::vector<FindChunk> find;
         for (size_t i = 0; i < go.size(); i++) {

@@ -31,6 +31,7 @@
 #include "ppg_device.h"
 #include "ppg_huffman.h"
 #include <atomic>
+#include <mutex>
 #define PPG_SORT_SLOT 320   // u16 per wave in global scratch: litlen sorted symbols 288, distance 32
 
 // CreateIndex pass 1 (IX): each job's output lives in a ring of 64 Ki positions of the out buffer
@@ -1266,22 +1267,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     }
 }
 
-// per-launch scratch of the sorted-symbol tables, stream-ordered: no device-wide sync, and the
-// device's default pool keeps the memory between launches (release threshold raised once)
+// per-launch scratch of the sorted-symbol tables, stream-ordered: no device-wide sync.  From a private
+// memory pool per device whose release threshold keeps the memory between launches (the
+// threshold used to be raised on the device's DEFAULT pool -- process-wide state that every other
+// hipMallocAsync user of the process then inherited); the default pool, untouched, only if a private
+// pool cannot be made.
 static hipError_t gsort_alloc(hipStream_t s, int njobs, uint16_t **p) {
-    static std::atomic<uint64_t> pools_set{0};
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    static bool tried[64] = {};
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (dev < 64 && !(pools_set.load() >> dev & 1)) {
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-            uint64_t t = ~0ull;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &t);
+    const size_t bytes = (size_t)njobs * PPG_SORT_SLOT * sizeof(uint16_t);
+    hipMemPool_t pool = nullptr;
+    if (dev >= 0 && dev < 64) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!tried[dev]) {
+            tried[dev] = true;
+            hipMemPoolProps props = {};
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            if (hipMemPoolCreate(&pools[dev], &props) == hipSuccess) {
+                uint64_t t = ~0ull;
+                (void)hipMemPoolSetAttribute(pools[dev], hipMemPoolAttrReleaseThreshold, &t);
+            } else {
+                pools[dev] = nullptr;
+                (void)hipGetLastError();
+            }
         }
-        pools_set.fetch_or(1ull << dev);
+        pool = pools[dev];
     }
-    return hipMallocAsync((void **)p, (size_t)njobs * PPG_SORT_SLOT * sizeof(uint16_t), s);
+    if (pool) return hipMallocFromPoolAsync((void **)p, bytes, pool, s);
+    return hipMallocAsync((void **)p, bytes, s);
 }
 #define PPG_GSORT_BEGIN(s, njobs)                          \
     uint16_t *gsort = nullptr;                             \

@@ -142,7 +142,7 @@ extern "C" __global__ __launch_bounds__(256) void ppg_pack_segs(const PpgPackSeg
             if (nw)
                 for (uint64_t i = 16 * w1 - d0 + threadIdx.x; i < len; i += 256) dst[d0 + i] = (uint8_t)seg_raw(s, s.a + i);
         }
-        // descriptors, rebased (u32 arithmetic: a half stays under 4 GiB)
+        // descriptors, rebased (u32 arithmetic: a half stays under 4 GiB -- half_max() refuses longer ones)
         const uint64_t nv = 4 * (uint64_t)s.nrec;
         const uint64_t pv = (nv + gridDim.x - 1) / gridDim.x;
         const uint64_t va = min(nv, (uint64_t)blockIdx.x * pv), vz = min(nv, (uint64_t)(blockIdx.x + 1) * pv);
@@ -432,6 +432,29 @@ namespace {
 using Clock = std::chrono::steady_clock;
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
 
+// Test hook (tests only), in the style of PPG_IX_PERTURB: PPG_PAIRS_PERTURB=short
+// takes one pair chunk off the last output batch's deduplicated record range (so no batch can ever
+// complete the last pair chunks: the no-progress guards of emit_next_local / emit_next_fused must
+// end the emission), =bases leaves make_segs without record bases (every segment search fails).
+// A guard that fires under the hook says so on stderr, so a test can tell which one ended it.
+int pairs_perturb() {
+    const char *e = getenv("PPG_PAIRS_PERTURB");
+    if (!e) return 0;
+    return !strcmp(e, "short") ? 1 : !strcmp(e, "bases") ? 2 : 0;
+}
+void guard_note(const char *where) {
+    if (pairs_perturb()) fprintf(stderr, "[ppg_pairs] PPG_DATA_ERROR at %s\n", where);
+}
+
+// A pair chunk half's descriptors are u32 positions relative to the half (ppg_pack_segs), so a half
+// must stay below 4 GiB: longer halves are refused with PPG_UNSUPPORTED before packing.
+// PPG_PAIR_HALF_MAX (tests only) lowers the limit so small inputs reach the refusal.
+int64_t half_max() {
+    const char *e = getenv("PPG_PAIR_HALF_MAX");
+    const int64_t v = e ? strtoll(e, nullptr, 10) : 0;
+    return v > 0 && v < (int64_t)UINT32_MAX ? v : (int64_t)UINT32_MAX;
+}
+
 // shard record number of this rank's deduplicated record d (skip the duplicates at or before it)
 int64_t shard_rec(const std::vector<int64_t> &dp, int64_t d) {
     return d + (int64_t)(std::upper_bound(dp.begin(), dp.end(), d) - dp.begin());
@@ -456,18 +479,18 @@ bool make_segs(const ppg_pairs *p, int f, int64_t d0, int64_t d1, int32_t grp, s
     const ppg_shard *sh = E.sh[f];
     const auto &B = sh->h_base;
     // chunks whose record bases are set (emit_run: the batches run so far; the rest are still 0)
-    const auto Bend = B.begin() + std::min<std::ptrdiff_t>((std::ptrdiff_t)B.size(), E.kvalid[f]);
+    const auto Bend = B.begin() + std::min<std::ptrdiff_t>((std::ptrdiff_t)B.size(), pairs_perturb() == 2 ? 0 : E.kvalid[f]);
     const auto &pos = E.pos[f];
     int64_t d = d0;
     while (d < d1) {
         const int64_t r = shard_rec(p->dp[f], d);
         const int32_t k = (int32_t)(std::upper_bound(B.begin(), Bend, r) - B.begin()) - 1;
-        if (k < 0) return false;
+        if (k < 0) { guard_note("make_segs (no chunk with a record base holds the record)"); return false; }
         const int64_t cend = B[(size_t)k] + (int64_t)sh->h_info[(size_t)k].records;
         const auto nd = std::upper_bound(pos.begin(), pos.end(), r);
         const int64_t stop = std::min<int64_t>(cend, nd == pos.end() ? INT64_MAX : *nd);
         const int64_t run = std::min(stop - r, d1 - d);
-        if (run <= 0) return false;
+        if (run <= 0) { guard_note("make_segs (no progress)"); return false; }
         const PpgInflateJob &J = sh->h_jobs[(size_t)k];
         PpgPackSeg g{};
         g.off = sh->offs.p + E.offst[f][(size_t)k];
@@ -585,6 +608,10 @@ int pack_window(ppg_pairs *p, int64_t e, int64_t J, int64_t pairs, Clock::time_p
             J2++;
         }
     }
+    // a half's descriptors are u32 positions relative to it (ppg_pack_segs)
+    for (int f = 0; f < 2; f++)
+        for (int64_t i = 0; i < J2 - e; i++)
+            if (hb[f][(size_t)i] > half_max()) return PPG_UNSUPPORTED;
     // 3. place and pack both files' halves of pair chunks [e, J2)
     for (int f = 0; f < 2; f++) {
         hipStream_t s = shard_stream(E.sh[f]);
@@ -656,6 +683,7 @@ int carry_rest(ppg_pairs *p, int f, int64_t cend, int32_t b) {
         add += (int64_t)(g.b - g.a);
         nadd += g.nrec;
     }
+    if (E.clen[f] + add > half_max()) return PPG_UNSUPPORTED;   // the carry starts a half (u32 descriptors)
     if (int rc = grow_keep(E.cbytes[f], (size_t)(E.clen[f] + add) + 64, s, (size_t)E.clen[f])) return rc;
     if (int rc = grow_keep(E.cdesc[f], 4 * (size_t)(E.cnrec[f] + nadd) + 4, s, 4 * (size_t)E.cnrec[f])) return rc;
     if (int rc = seg_pack(E, seg, E.cbytes[f].p, E.cdesc[f].p, s)) return rc;
@@ -687,7 +715,10 @@ int emit_next_local(ppg_pairs *p, int64_t *j0, int64_t *j1) {
             const int64_t c2 = e * K + E.cnrec[f];
             int32_t nb = 0;
             while ((size_t)nb + 1 < E.bhi[f].size() && E.bhi[f][(size_t)nb] <= c2) nb++;
-            if (nb == b) return PPG_DATA_ERROR;   // no progress: the batches cannot complete the pair chunk
+            if (nb == b) {   // no progress: the batches cannot complete the pair chunk
+                guard_note("emit_next_local (no batch completes the pair chunk)");
+                return PPG_DATA_ERROR;
+            }
             E.batch[f] = nb;
             run[f] = true;
         }
@@ -755,6 +786,8 @@ int fused_collected(ppg_pairs *p, int f, int32_t b) {
     }
     E.blo[f].push_back(dedup_of(E.pos[f], r0));
     E.bhi[f].push_back(dedup_of(E.pos[f], r1));
+    if (pairs_perturb() == 1 && (size_t)b + 1 == sh->batches.size())
+        E.bhi[f].back() = std::max(E.blo[f].back(), E.bhi[f].back() - E.K);
     E.kvalid[f] = b1;
     if ((size_t)b + 1 == sh->batches.size()) {
         const int rc = shard_finish(sh, E.run_ms[f]);
@@ -827,7 +860,10 @@ int emit_next_fused(ppg_pairs *p, int64_t *j0, int64_t *j1) {
             const int64_t cend = e * K + E.cnrec[f];
             const int32_t b = E.batch[f];
             if (b >= 0 && E.blo[f][(size_t)b] <= cend && E.bhi[f][(size_t)b] >= need) continue;
-            if (E.done[f]) return PPG_DATA_ERROR;   // every batch has run and the pair chunk is not complete
+            if (E.done[f]) {   // every batch has run and the pair chunk is not complete
+                guard_note("emit_next_fused (every batch has run, the pair chunk is incomplete)");
+                return PPG_DATA_ERROR;
+            }
             if (int rc = carry_rest(p, f, cend, b)) return rc;
             run[f] = true;
         }
@@ -892,6 +928,9 @@ int emit_exchange(ppg_pairs *p, int64_t *j0, int64_t *j1) {
             piece_len[f][(size_t)pl[i].grp] += (int64_t)(seg[i].b - seg[i].a);
             piece_rec[(size_t)pl[i].grp] += seg[i].nrec;
         }
+        for (int64_t L : piece_len[f])   // a piece lies in one half (u32 descriptors): joins the status gather
+            if (L > half_max()) status = PPG_UNSUPPORTED;
+        if (status != PPG_OK) break;
         // owner groups: pieces back to back, each group padded to 8 bytes (int64 words)
         std::vector<int64_t> poff((size_t)np), proff((size_t)np);
         int64_t gb = 0, gr = 0;
@@ -1009,6 +1048,9 @@ int emit_exchange(ppg_pairs *p, int64_t *j0, int64_t *j1) {
             E.blen[f][(size_t)pj[i]] += (int64_t)seg[i].b;
             E.rcnt[f][(size_t)pj[i]] += seg[i].nrec;
         }
+        // (after the exchange, which every rank joined: a refusal here strands no one)
+        for (int64_t L : E.blen[f])
+            if (L > half_max()) return PPG_UNSUPPORTED;
         int64_t bo = 0, ro = 0;
         for (int64_t j = 0; j < nj; j++) {
             E.boff[f][(size_t)j] = bo;
@@ -1161,6 +1203,8 @@ int ppg_pairs_emit_begin(ppg_pairs *p, ppg_shard *r1, ppg_shard *r2, ppg_comm *c
         // the windows' deduplicated numbering is this rank's: pairs beyond either file's records do not exist
         for (int f = 0; f < 2; f++)
             if (E.bhi[f].empty() ? p->res.pairs > 0 : E.bhi[f].back() < p->res.pairs) return PPG_ARG_ERROR;
+        if (pairs_perturb() == 1)
+            for (int f = 0; f < 2; f++) E.bhi[f].back() = std::max(E.blo[f].back(), E.bhi[f].back() - E.K);
     } else {
         if (p->st[0].size() != (size_t)nranks + 1 || p->st[1].size() != (size_t)nranks + 1) return PPG_ARG_ERROR;
         E.j_lo = E.j_hi = 0;   // set by the exchange

@@ -193,6 +193,8 @@ class PairedFASTQ:
         self.result = self._pairs.check(self.shards[0], self.shards[1])
         self.pairs = require_pairs(self.result)
         self.window_bytes = window_bytes
+        self._it = None          # the emission pair_chunk() advances (random access)
+        self._win = (0, 0)       # its current window [j0, j1)
 
     def Count(self):
         return self.pairs
@@ -203,18 +205,31 @@ class PairedFASTQ:
 
     def pair_chunks(self):
         """Yield (j, R1 records, R2 records) for every pair chunk in order."""
+        self._it, self._win = None, (0, 0)   # this emission replaces pair_chunk()'s
         for j0, j1 in self._pairs.emit(self.shards[0], self.shards[1], self.K, window_bytes=self.window_bytes):
             for j in range(j0, j1):
                 yield (j,) + tuple(records_from_descriptors(*self._pairs.copy_chunk(j, f)) for f in (0, 1))
 
     def pair_chunk(self, j):
-        """(R1 records, R2 records) of pair chunk j: pairs [j*K, min((j+1)*K, Count))."""
+        """(R1 records, R2 records) of pair chunk j: pairs [j*K, min((j+1)*K, Count)).  Only chunk j
+        is copied out: the emission's windows are advanced (not copied) until one holds j, and kept
+        for the next call, so ascending calls walk the windows once (every earlier pair
+        chunk was copied and parsed before, O(j) per call); a j behind the current window restarts
+        the emission (multi-batch shards re-run their batches)."""
         if not 0 <= j < self.chunks:
             raise IndexError(j)
-        for jj, a, b in self.pair_chunks():
-            if jj == j:
-                return a, b
-        raise IndexError(j)
+        j0, j1 = self._win
+        if not (j0 <= j < j1):
+            if self._it is None or j < j0:
+                self._it = self._pairs.emit(self.shards[0], self.shards[1], self.K, window_bytes=self.window_bytes)
+            for w in self._it:
+                self._win = w
+                if w[0] <= j < w[1]:
+                    break
+            else:
+                self._it, self._win = None, (0, 0)
+                raise IndexError(j)
+        return tuple(records_from_descriptors(*self._pairs.copy_chunk(j, f)) for f in (0, 1))
 
     def __iter__(self):
         for _, a, b in self.pair_chunks():

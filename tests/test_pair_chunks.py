@@ -18,6 +18,7 @@ import pytest
 import parallelparsing_amd as pp
 from oracle import oracle as O
 from parallelparsing_amd import paired
+from parallelparsing_amd import _lib
 
 pytestmark = pytest.mark.gpu
 
@@ -329,3 +330,104 @@ def test_pair_chunks_multi_rank_on_one_gpu(pair_files, world, K):
         for f in (0, 1):
             eb, ed = expected_half(recs[f][0], lo, hi)
             assert halves[f] == (hashlib.sha256(eb).hexdigest(), hashlib.sha256(ed.tobytes()).hexdigest(), hi - lo), (j, f)
+
+
+def _maxrss_mb():
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+
+
+@pytest.mark.parametrize("form,perturb,guard", [("begin", "short", "emit_next_local"),
+                                                ("run", "short", "emit_next_fused"),
+                                                ("begin", "bases", "make_segs"),
+                                                ("run", "bases", "make_segs")])
+def test_no_progress_guards_end_the_emission(pair_files, device, capfd, monkeypatch, form, perturb, guard):
+    """VERDICT r05 next #4 (the r05k memory-cap kill: a segment search that found no progress grew
+    its list without end).  PPG_PAIRS_PERTURB (a test hook) makes the last output batch one pair chunk
+    short of its records ("short": no batch can ever complete the last pair chunks) or leaves the
+    segment search without record bases ("bases"); both emission forms must end with PPG_DATA_ERROR,
+    promptly and in bounded host memory, at the guard named on stderr -- emit_next_local's "no batch
+    completes the pair chunk" (ppg_pairs.hip, after carry_rest), emit_next_fused's "every batch has
+    run", make_segs' "no record base"."""
+    import time
+    gz, chunks, recs, nrec = pair_files
+    ix = [pp.Core.BuildDeflateIndex(g, c) for g, c in zip(gz, chunks)]
+    cap = 3 << 20   # multi-batch shards: windows cross batches
+    if form == "begin":
+        sh = [shard_of(g, i, device, cap) for g, i in zip(gz, ix)]
+        pr = paired.Pairs()
+        assert pr.check(sh[0], sh[1])["mismatches"] == 0
+    else:
+        sh = []
+        for g, i in zip(gz, ix):
+            _, i0, _, _ = i.point_fields(0)
+            _, i1, _, _ = i.point_fields(i.Count - 1)
+            s_ = pp.Shard(i, np.frombuffer(g[i0 - 1:i1], np.uint8), 0, i.Count - 1, device=device, out_capacity=cap)
+            paired.attach_keys(s_, 400_000)
+            sh.append(s_)
+        pr = paired.Pairs()
+    assert sh[0].batches >= 3
+    monkeypatch.setenv("PPG_PAIRS_PERTURB", perturb)
+    rss0, t = _maxrss_mb(), time.time()
+    windows = 0
+    with pytest.raises(pp.PpgError) as ei:
+        # one pair chunk per window (window_bytes=1): a finished file's last window would otherwise
+        # reach its last record through the pair count, past the shortened range
+        it = pr.emit(sh[0], sh[1], 2500, window_bytes=1) if form == "begin" else \
+            pr.emit_run(sh[0], sh[1], 2500, window_bytes=1)
+        for _ in it:
+            windows += 1
+            assert windows < 20
+    assert ei.value.code == _lib.PPG_DATA_ERROR
+    assert time.time() - t < 60 and _maxrss_mb() - rss0 < 512
+    err = capfd.readouterr().err
+    assert f"[ppg_pairs] PPG_DATA_ERROR at {guard}" in err, err[-2000:]
+    if perturb == "short":
+        assert windows >= 1   # the earlier pair chunks were emitted; the last ones cannot be
+    # the hook off: the same shards emit every pair chunk again
+    monkeypatch.delenv("PPG_PAIRS_PERTURB")
+    if form == "run":
+        for _ in pr.emit_run(sh[0], sh[1], 2500):
+            pass
+        assert pr.check(sh[0], sh[1])["pairs"] == nrec
+    seen = set()
+    for j0, j1 in pr.emit(sh[0], sh[1], 2500):
+        check_window(pr, j0, j1, 2500, recs, nrec, seen)
+    assert seen == set(range(-(-nrec // 2500)))
+
+
+@pytest.mark.parametrize("form", ["begin", "run", "carry"])
+def test_half_of_4gib_or_more_is_refused(pair_files, device, monkeypatch, form):
+    """a pair chunk half's descriptors are u32 positions relative to the half,
+    so a half of 4 GiB or more must be refused (PPG_UNSUPPORTED), never wrapped.  PPG_PAIR_HALF_MAX
+    (a test hook) lowers the 4 GiB limit to 1 MB so the 30,000-record files reach it: one pair chunk
+    of every pair (~11.5 MB per half) is refused in both emission forms, and with multi-batch shards
+    the carried first part of a half is refused too; pair chunks under the limit still emit."""
+    gz, chunks, recs, nrec = pair_files
+    ix = [pp.Core.BuildDeflateIndex(g, c) for g, c in zip(gz, chunks)]
+    cap = (3 << 20) if form == "carry" else 0
+    monkeypatch.setenv("PPG_PAIR_HALF_MAX", str(1 << 20))
+    if form == "run":
+        sh = []
+        for g, i in zip(gz, ix):
+            _, i0, _, _ = i.point_fields(0)
+            _, i1, _, _ = i.point_fields(i.Count - 1)
+            s_ = pp.Shard(i, np.frombuffer(g[i0 - 1:i1], np.uint8), 0, i.Count - 1, device=device)
+            paired.attach_keys(s_, 400_000)
+            sh.append(s_)
+        pr = paired.Pairs()
+        it = pr.emit_run(sh[0], sh[1], 10 * nrec)
+    else:
+        sh = [shard_of(g, i, device, cap) for g, i in zip(gz, ix)]
+        pr = paired.Pairs()
+        pr.check(sh[0], sh[1])
+        it = pr.emit(sh[0], sh[1], 10 * nrec)
+    with pytest.raises(pp.PpgError) as ei:
+        next(it)
+    assert ei.value.code == _lib.PPG_UNSUPPORTED
+    # ~2,700 records (~1 MB) per half fit the lowered limit
+    if form != "run":
+        seen = set()
+        for j0, j1 in pr.emit(sh[0], sh[1], 2000):
+            check_window(pr, j0, j1, 2000, recs, nrec, seen)
+        assert seen == set(range(-(-nrec // 2000)))

@@ -62,13 +62,20 @@ def test_paired_fastq_pairs(tmp_path):
     pf = paired.PairedFASTQ(ix1, p1, ix2, p2, pair_chunk=4000)
     assert pf.Count() == nrec and pf.chunks == 8
     recs1 = t1.split(b"\n")
-    for j in (0, 3, 7):
+    # random access (only chunk j copied out; ascending calls walk the windows once,
+    # a chunk behind the current window restarts the emission), then the iteration agrees
+    pf.window_bytes = 3 << 20   # several windows
+    for j in (0, 3, 7, 5, 5, 1):
         a, b = pf.pair_chunk(j)
         assert len(a) == len(b) == min(4000, nrec - 4000 * j)
         for i in (0, len(a) // 2, len(a) - 1):
             g = 4000 * j + i
             assert a[i].identifier == recs1[4 * g][1:]
             assert a[i].identifier.split(b".")[:2] == b[i].identifier.split(b".")[:2]
+    it = {j: ([r.identifier for r in a], [r.sequence for r in b]) for j, a, b in pf.pair_chunks() if j in (2, 6)}
+    for j in (2, 6):
+        a2, b2 = pf.pair_chunk(j)
+        assert ([r.identifier for r in a2], [r.sequence for r in b2]) == it[j]
 
 
 @pytest.mark.gpu

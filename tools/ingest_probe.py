@@ -1,0 +1,121 @@
+"""Where the ingest leg's time goes (one 8 GiB piece's read + copy took 299 ms
+against ~175 ms for the others, in every run).  Builds the bench member, writes it to $TMPDIR as the
+bench's ingest leg does, reports on which NUMA node the file's page-cache pages sit (one page per
+64 MiB, faulted in through a read-only mapping and asked with move_pages(2), no migration) per piece,
+then runs ppg_file_decompress_all twice with PPG_INGEST_VERBOSE=1 (pread vs pinned-slot waits per
+piece on stderr) and the pinned -> device copy rate.
+
+  python tools/ingest_probe.py [--seg-records N] [--repeats R] [--piece-gib G] [--variant v ...]
+"""
+import argparse
+import ctypes as C
+import json
+import mmap
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SYS_move_pages = 279   # x86_64
+
+
+def page_nodes(path, step=64 << 20):
+    """(offset, node) for one page per `step` bytes of the file's page cache."""
+    libc = C.CDLL(None, use_errno=True)
+    libc.syscall.restype = C.c_long
+    size = os.path.getsize(path)
+    out = []
+    with open(path, "rb") as f:
+        m = mmap.mmap(f.fileno(), size, prot=mmap.PROT_READ)
+        # the mapping's address (ctypes cannot take a read-only mmap's buffer): from /proc/self/maps
+        m_addr = None
+        with open("/proc/self/maps") as mp:
+            for ln in mp:
+                if path in ln:
+                    a, b = (int(x, 16) for x in ln.split()[0].split("-"))
+                    if b - a >= size - 4096:
+                        m_addr = a
+                        break
+        if m_addr is None:
+            return {"error": "mapping not found"}
+        offs = list(range(0, size, step))
+        for o in offs:
+            m[o]   # fault the page in (a read-only mapping of the page-cache page)
+        n = len(offs)
+        pages = (C.c_void_p * n)(*[m_addr + o for o in offs])
+        status = (C.c_int * n)()
+        rc = libc.syscall(SYS_move_pages, 0, C.c_ulong(n), pages, None, status, 0)
+        if rc != 0:
+            return {"error": f"move_pages rc {rc} errno {C.get_errno()}"}
+        out = list(zip(offs, list(status)))
+        m.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seg-records", type=int, default=10_485_760)
+    ap.add_argument("--repeats", type=int, default=51)
+    ap.add_argument("--piece-gib", type=float, default=8.0)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--runs", type=int, default=2)
+    args = ap.parse_args()
+    import parallelparsing_amd as pp
+    from parallelparsing_amd.tiled import TiledFile
+    t = time.time()
+    tf = TiledFile(args.seg_records, args.repeats, 10000, threads=16)
+    print(f"[probe] member built in {time.time() - t:.1f}s: {tf.file_len / 1e9:.2f} GB", file=sys.stderr, flush=True)
+    path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"ppg_probe_{os.getpid()}.fastq.gz")
+    res = {}
+    try:
+        t = time.perf_counter()
+        with open(path, "wb") as f:
+            for lo in range(0, tf.file_len, 1 << 30):
+                f.write(tf.file_bytes(lo, min(tf.file_len, lo + (1 << 30))))
+        res["write_s"] = time.perf_counter() - t
+        nodes = page_nodes(path)
+        if isinstance(nodes, dict):
+            res["numa"] = nodes
+        else:
+            pb = int(args.piece_gib * (1 << 30))
+            per = {}
+            for o, nd in nodes:
+                per.setdefault(o // pb, {}).setdefault(str(nd), 0)
+                per[o // pb][str(nd)] += 1
+            res["numa_pages_per_piece"] = per
+            print(f"[probe] page-cache nodes per {args.piece_gib:g} GiB piece: {per}", file=sys.stderr, flush=True)
+        ix = tf.index(0, tf.npoints)
+        dev = pp.Device(0)
+        os.environ["PPG_INGEST_VERBOSE"] = "1"
+        runs = []
+        for _ in range(args.runs):
+            _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=args.threads, piece_bytes=int(args.piece_gib * (1 << 30)))
+            assert tot == tf.expected_records()
+            runs.append(sec)
+            print(f"[probe] run: {sec:.3f} s, {tot / sec / 1e6:.1f} M records/s", file=sys.stderr, flush=True)
+        res["runs_s"] = runs
+        dev.release_file_buffers()
+        import torch
+        n = 4 << 30
+        h = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        d = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        best = 0.0
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            d.copy_(h, non_blocking=True)
+            torch.cuda.synchronize()
+            best = max(best, n / (time.perf_counter() - t) / 1e9)
+        res["pcie_h2d_GBps"] = best
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
