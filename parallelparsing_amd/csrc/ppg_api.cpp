@@ -36,6 +36,7 @@ size_t ppg_inflate_lds_bytes(int ring_bits, int lit_bits);
 hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const uint32_t *comp, uint64_t nwords,
                               const PpgInflateJob *jobs, const uint8_t *dicts, uint8_t *out, PpgInflateResult *res,
                               int njobs, uint32_t *nls);
+hipError_t ppg_launch_total_to_host(hipStream_t s, const uint64_t *total, uint64_t *host);
 hipError_t ppg_launch_parse_count(hipStream_t s, const uint8_t *out, const PpgInflateJob *jobs,
                                   const PpgInflateResult *ires, const uint8_t *offs, const PpgOffsetRef *oref,
                                   PpgParseInfo *info, uint64_t *base, uint64_t *total, int n, const uint32_t *nls);
@@ -681,7 +682,7 @@ int batch_launch(ppg_shard *sh, int32_t b0, int32_t b1) {
     HIPCHK(hipEventRecord(sh->ev[1], s));
     HIPCHK(ppg_launch_parse_count(s, sh->out.p, sh->jobs.p + b0, sh->res.p + b0, sh->offs.p, sh->oref.p + b0,
                                   sh->info.p + b0, sh->base.p + b0, sh->total.p, nb, sh->nls.p));
-    HIPCHK(hipMemcpyAsync(sh->h_tot, sh->total.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(ppg_launch_total_to_host(s, sh->total.p, sh->h_tot));   // (a kernel store: no DMA engine, ppg_parse.hip)
     HIPCHK(hipEventRecord(sh->ev[2], s));
     // descriptors at the batch's shard-global record base (sh->total_records: batches of one shard
     // run one after the other), writes bounded by the buffer
@@ -1061,13 +1062,18 @@ bool pread_parallel(int fd, uint8_t *dst, int64_t off, int64_t len, int threads)
     return true;
 }
 
-constexpr int kSlots = 4;     // pinned staging slots
+constexpr int kSlots = 16;    // pinned staging slots at most (IngestState::nslots are used)
 constexpr int kPieces = 3;   // device piece slots: one finishing, one decoding, one filling
-constexpr int64_t kSlotBytes = (int64_t)128 << 20;
 
 struct IngestState {
+    // staging shape, fixed when the state is made: 4 slots of 128 MB on one copy stream by default;
+    // PPG_INGEST_SLOTS / PPG_INGEST_SLOT_MB / PPG_INGEST_COPY_STREAMS (1-2) for A/B runs (tools/ingest_probe.py)
+    int nslots = 4, ncs = 1;
+    int64_t slot_bytes = (int64_t)128 << 20;
     PinnedBuf slot[kSlots];       // pinned host staging, streamed through round-robin
     hipEvent_t slot_ev[kSlots] = {};
+    hipStream_t cs2 = nullptr;    // a second copy stream (ncs == 2): odd slots
+    hipEvent_t join_ev = nullptr; // cs2's copies of a piece, joined into cs before the piece's event
     DevBuf<uint8_t> db[kPieces];  // device copies of pieces
     hipStream_t cs = nullptr;     // copy stream
     hipStream_t ks[kPieces] = {};   // decode streams, one per piece slot
@@ -1079,6 +1085,8 @@ static void ingest_free(IngestState *st) {
     if (!st) return;
     for (int i = 0; i < kSlots; i++)
         if (st->slot_ev[i]) (void)hipEventDestroy(st->slot_ev[i]);
+    if (st->join_ev) (void)hipEventDestroy(st->join_ev);
+    if (st->cs2) (void)hipStreamDestroy(st->cs2);
     for (int i = 0; i < kPieces; i++) {
         if (st->sh[i]) ppg_shard_free(st->sh[i]);
         if (st->piece_ev[i]) (void)hipEventDestroy(st->piece_ev[i]);
@@ -1138,7 +1146,8 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
 
     // pieces: consecutive chunks of about piece_bytes compressed bytes (at least one chunk).
     // (Ramping the first / last pieces down measured slower: one chunk alone takes ~100 ms, so
-    // small pieces neither start nor drain the GPU faster.)
+    // small pieces neither start nor drain the GPU faster; r06, with the last pieces split at side
+    // points: 1.45-1.50 vs 1.34-1.36 s, 1.10 vs 1.09 s per 50 GB member, tools/ingest_probe.py.)
     std::vector<std::pair<int32_t, int32_t>> pieces;
     int64_t maxlen = 0;
     for (int32_t a = 0; a < n;) {
@@ -1157,10 +1166,32 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
     if (!ctx->ingest) {
         auto st = new IngestState;
         ctx->ingest = st;
-        HIPCHK(hipStreamCreateWithFlags(&st->cs, hipStreamNonBlocking));
-        for (int i = 0; i < kSlots; i++) {
+        auto env_int = [](const char *k, int64_t d, int64_t lo, int64_t hi) {
+            const char *e = getenv(k);
+            return e ? std::min(hi, std::max(lo, (int64_t)strtoll(e, nullptr, 10))) : d;
+        };
+        st->nslots = (int)env_int("PPG_INGEST_SLOTS", 4, 2, kSlots);
+        st->slot_bytes = env_int("PPG_INGEST_SLOT_MB", 128, 8, 1024) << 20;
+        st->ncs = (int)env_int("PPG_INGEST_COPY_STREAMS", 1, 1, 2);
+        // the copy stream at the greatest priority, i.e. on a hardware queue of its own: a stream
+        // sharing a queue with a decode stream runs in order behind its kernels, and the piece copies
+        // then wait for a whole decode (r06: one ~131 ms stall per 50 GB ingest whenever the runtime,
+        // GPU_MAX_HW_QUEUES = 4, mapped the copy stream onto a piece stream's queue; gone at the
+        // greatest priority or with 8 queues -- tools/ingest_probe.py).  PPG_INGEST_COPY_PRIO=0: off.
+        if (env_int("PPG_INGEST_COPY_PRIO", 1, 0, 1)) {
+            int lo = 0, hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHK(hipStreamCreateWithPriority(&st->cs, hipStreamNonBlocking, hi));
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&st->cs, hipStreamNonBlocking));
+        }
+        if (st->ncs == 2) {
+            HIPCHK(hipStreamCreateWithFlags(&st->cs2, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&st->join_ev, hipEventDisableTiming));
+        }
+        for (int i = 0; i < st->nslots; i++) {
             HIPCHK(hipEventCreateWithFlags(&st->slot_ev[i], hipEventDisableTiming));
-            HIPCHK(st->slot[i].alloc((size_t)kSlotBytes));
+            HIPCHK(st->slot[i].alloc((size_t)st->slot_bytes));
         }
         for (int i = 0; i < kPieces; i++) {
             st->sh[i] = new ppg_shard;
@@ -1202,9 +1233,10 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             int64_t off, len;
             range(k, off, len);
             uint8_t *dst = S.db[k % kPieces].p;
-            double wait_ms = 0, read_ms = 0, slow_ms = 0;   // (PPG_INGEST_VERBOSE) slot waits, preads, slowest pread
-            for (int64_t r = 0; r < len && rcp == PPG_OK; r += kSlotBytes, slot = (slot + 1) % kSlots) {
-                const int64_t m = std::min(kSlotBytes, len - r);
+            double wait_ms = 0, read_ms = 0, slow_ms = 0, enq_ms = 0;   // (PPG_INGEST_VERBOSE) slot waits, preads, slowest pread, copy enqueues
+            for (int64_t r = 0; r < len && rcp == PPG_OK; r += S.slot_bytes, slot = (slot + 1) % S.nslots) {
+                const int64_t m = std::min(S.slot_bytes, len - r);
+                hipStream_t cs = S.ncs == 2 && (slot & 1) ? S.cs2 : S.cs;
                 const double tw = verbose ? now_ms() : 0;
                 if (hipEventSynchronize(S.slot_ev[slot]) != hipSuccess) { rcp = PPG_DEVICE_ERROR; break; }
                 const double tr = verbose ? now_ms() : 0;
@@ -1215,17 +1247,27 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
                     read_ms += te - tr;
                     slow_ms = std::max(slow_ms, te - tr);
                 }
-                if (hipMemcpyAsync(dst + r, S.slot[slot].p, (size_t)m, hipMemcpyHostToDevice, S.cs) != hipSuccess ||
-                    hipEventRecord(S.slot_ev[slot], S.cs) != hipSuccess)
+                const double tq = verbose ? now_ms() : 0;
+                if (hipMemcpyAsync(dst + r, S.slot[slot].p, (size_t)m, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                    hipEventRecord(S.slot_ev[slot], cs) != hipSuccess)
                     rcp = PPG_DEVICE_ERROR;
+                if (verbose) {
+                    const double dq = now_ms() - tq;
+                    enq_ms += dq;
+                    if (dq > 5) fprintf(stderr, "[ingest] piece %zu: a copy's enqueue took %.1f ms at %.1f ms\n", k, dq, tq);
+                    if (tr - tw > 20) fprintf(stderr, "[ingest] piece %zu: slot %zu waited %.1f ms at %.1f ms\n", k, slot, tr - tw, tw);
+                }
             }
+            if (rcp == PPG_OK && S.ncs == 2 &&
+                (hipEventRecord(S.join_ev, S.cs2) != hipSuccess || hipStreamWaitEvent(S.cs, S.join_ev, 0) != hipSuccess))
+                rcp = PPG_DEVICE_ERROR;
             if (rcp == PPG_OK && (hipMemsetAsync(dst + len, 0, 64, S.cs) != hipSuccess ||
                                   hipEventRecord(S.piece_ev[k % kPieces], S.cs) != hipSuccess))
                 rcp = PPG_DEVICE_ERROR;
             if (verbose)
                 fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms (pread %.1f ms, slowest "
-                        "128 MB %.1f ms; waiting for pinned slots %.1f ms)\n", k, len / 1e6, t1, now_ms() - t1, read_ms,
-                        slow_ms, wait_ms);
+                        "128 MB %.1f ms; waiting for pinned slots %.1f ms; copy enqueues %.1f ms)\n", k, len / 1e6, t1,
+                        now_ms() - t1, read_ms, slow_ms, wait_ms, enq_ms);
             std::lock_guard<std::mutex> lk(mu);
             if (rcp != PPG_OK) prod_rc = rcp;
             else ready = k + 1;
@@ -1246,8 +1288,13 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
     auto collect = [&](size_t k) -> int {
         ppg_shard *sh = S.sh[k % kPieces];
         float ms = 0;
+        const double tc = now_ms();
         int r = batch_collect(sh, 0, sh->n, ms);
+        const double tc1 = now_ms();
         if (r == PPG_OK) r = shard_finish(sh, ms);
+        if (verbose)
+            fprintf(stderr, "[ingest] piece %zu: collect from %.1f ms: batch_collect %.1f ms, finish %.1f ms\n", k, tc,
+                    tc1 - tc, now_ms() - tc1);
         const int32_t a = pieces[k].first, b = pieces[k].second;
         if (verbose)
             fprintf(stderr, "[ingest] piece %zu: %d chunks collected at %.1f ms (kernels %.1f)\n", k, b - a, now_ms(),
@@ -1277,18 +1324,23 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
         if (hipStreamWaitEvent(S.ks[k % kPieces], S.piece_ev[k % kPieces], 0) != hipSuccess) { rc = PPG_DEVICE_ERROR; break; }
         rc = shard_prepare(sh, ix, first + pieces[k].first, pieces[k].second - pieces[k].first, S.db[k % kPieces].p, len,
                            0, S.ks[k % kPieces]);
+        const double tp1 = now_ms();
         if (rc == PPG_OK && split)
             rc = shard_split_from_index(sh, ix, first + pieces[k].first, pieces[k].second - pieces[k].first);
         if (rc != PPG_OK) break;
+        const double tp2 = now_ms();
         shard_reset(sh);
         rc = sh->batches.size() == 1 ? batch_launch(sh, 0, sh->n) : PPG_ARG_ERROR;
-        if (verbose) fprintf(stderr, "[ingest] piece %zu: prepared in %.1f ms, launched at %.1f ms\n", k, now_ms() - tp, now_ms());
+        if (verbose)
+            fprintf(stderr, "[ingest] piece %zu: prepared in %.1f ms (prepare %.1f, split %.1f, launch %.1f), launched at "
+                    "%.1f ms\n", k, now_ms() - tp, tp1 - tp, tp2 - tp1, now_ms() - tp2, now_ms());
         if (rc != PPG_OK) break;
         if (k > 0 && (rc = collect(k - 1)) != PPG_OK) break;
     }
     if (rc == PPG_OK && np > 0) rc = collect(np - 1);
     hipStream_t cs = S.cs;
     HIPCHK(hipStreamSynchronize(cs));
+    if (S.cs2) HIPCHK(hipStreamSynchronize(S.cs2));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (total_records) *total_records = total;
     if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

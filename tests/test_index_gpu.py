@@ -274,6 +274,26 @@ def test_file_ingest_uses_side_points(piece, tmp_path, device):
     assert (r0 == r1).all()
 
 
+def test_file_ingest_with_side_points_in_part_of_the_file(tmp_path, device):
+    """Host ingest with side points in only part of the file (the index's tail, its middle, or one
+    chunk): the chunks that have them are split, the others decoded whole, in pieces of several
+    sizes -- the same per-chunk records as the plain index."""
+    nrec = 160_000
+    gz = synth_gz(fastq_text(nrec, seed=34), level=6, piece=4 << 20)
+    p = tmp_path / "r.gz"
+    p.write_bytes(gz)
+    plain = pp.Core.BuildDeflateIndexGpu(gz, 5000, device=device)
+    side = pp.Core.BuildDeflateIndexGpu(gz, 5000, device=device, side_bytes=100_000)
+    n = plain.Count - 1
+    r0, t0, _ = pp.decompress_file(plain, str(p), piece_bytes=3 << 20, threads=4, device=device)
+    for c0, m in ((n // 2, n - n // 2), (n // 4, n // 2), (n - 3, 1)):
+        part = pp.Core.BuildDeflateIndexGpu(gz, 5000, device=device)
+        part.set_side_points(*side.side_points(c0, m))
+        for piece in (1 << 20, 3 << 20, 64 << 20):
+            r1, t1, _ = pp.decompress_file(part, str(p), piece_bytes=piece, threads=4, device=device)
+            assert t1 == t0 == nrec and (r0 == r1).all(), (c0, piece)
+
+
 @pytest.mark.parametrize("spares", ["0", "1", ""])
 def test_false_start_redos_speculative_and_serial(spares, device, monkeypatch):
     """false starts (finder candidates moved off their block starts by PPG_IX_PERTURB) are redone

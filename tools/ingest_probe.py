@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--piece-gib", type=float, default=8.0)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--runs", type=int, default=2)
+    ap.add_argument("--variant", nargs="*", default=["plain:INDEX=plain", "noprio:INDEX=plain,COPY_PRIO=0"],
+                    help="name:KEY=V,... -- INDEX=plain|tail, SLOTS, SLOT_MB, COPY_STREAMS (PPG_INGEST_*)")
     args = ap.parse_args()
     import parallelparsing_amd as pp
     from parallelparsing_amd.tiled import TiledFile
@@ -88,16 +90,30 @@ def main():
                 per[o // pb][str(nd)] += 1
             res["numa_pages_per_piece"] = per
             print(f"[probe] page-cache nodes per {args.piece_gib:g} GiB piece: {per}", file=sys.stderr, flush=True)
-        ix = tf.index(0, tf.npoints)
+        pb = int(args.piece_gib * (1 << 30))
+        plain = tf.index(0, tf.npoints)
+        tail = tf.index(0, tf.npoints)   # side points for the last 2 pieces' chunks (bench.py's ingest leg)
+        c0 = int(np.searchsorted(tf.p_input, tf.file_len - 2 * pb))
+        tail.set_side_points(*tf.side_points(c0, tf.npoints, 8))
         dev = pp.Device(0)
         os.environ["PPG_INGEST_VERBOSE"] = "1"
-        runs = []
-        for _ in range(args.runs):
-            _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=args.threads, piece_bytes=int(args.piece_gib * (1 << 30)))
-            assert tot == tf.expected_records()
-            runs.append(sec)
-            print(f"[probe] run: {sec:.3f} s, {tot / sec / 1e6:.1f} M records/s", file=sys.stderr, flush=True)
-        res["runs_s"] = runs
+        res["variants"] = {}
+        for spec in args.variant:
+            name, _, kv = spec.partition(":")
+            env = dict(x.split("=") for x in kv.split(",") if x)
+            ix = plain if env.pop("INDEX", "tail") == "plain" else tail
+            for k in ("PPG_INGEST_SLOTS", "PPG_INGEST_SLOT_MB", "PPG_INGEST_COPY_STREAMS", "PPG_INGEST_COPY_PRIO"):
+                os.environ.pop(k, None)
+            os.environ.update({"PPG_INGEST_" + k: v for k, v in env.items()})
+            dev.release_file_buffers()   # the staging shape is read when the buffers are made
+            runs = []
+            for _ in range(args.runs):
+                print(f"[probe] variant {name}", file=sys.stderr, flush=True)
+                _, tot, sec = pp.decompress_file(ix, path, device=dev, threads=args.threads, piece_bytes=pb)
+                assert tot == tf.expected_records()
+                runs.append(sec)
+                print(f"[probe] {name}: {sec:.3f} s, {tot / sec / 1e6:.1f} M records/s", file=sys.stderr, flush=True)
+            res["variants"][name] = runs
         dev.release_file_buffers()
         import torch
         n = 4 << 30
