@@ -1108,6 +1108,12 @@ def main():
     if args.seg_records is None:   # the paired files keep 1 GB segments: two members must fit one GPU
         args.seg_records = PAIRED_SEG_RECORDS if args.paired else SEG_RECORDS
 
+    # 8 hardware queues per process (the box exports HIP's default, 4): with 4, the runtime maps some
+    # of the library's streams onto one queue, where they run in order -- the host ingest's copy
+    # stream behind a piece's decode kernels (r06: the 50 GB ingest 1.24 -> 1.08 s, profiles/r06h_*;
+    # the library also puts that copy stream at the greatest priority).  Set before anything
+    # initialises HIP; the ranks a launch starts inherit it.
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("PPG_BENCH_HW_QUEUES", "8")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))

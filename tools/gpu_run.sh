@@ -68,8 +68,9 @@ run_step() {
     timeout -k 10 400 python3 -u bench.py --paired --steps 3 --warmup 1 $PAIRED_ARGS > $O/paired.json 2> $O/paired.log || return $?
     line $O/paired.json ;;
   w8)
+    # (r06: with the N > 1 end-to-end leg; --no-ingest in W8_ARGS skips it)
     PPG_BENCH_ONE_DEVICE=1 PPG_DIST_BACKEND=gloo timeout -k 10 900 python3 -u bench.py --gpus 8 --steps 2 --warmup 1 \
-      $NOLEGS $W8_ARGS $xa > $O/w8.json 2> $O/w8.log || { tail -20 $O/w8.log; return 1; }
+      --no-cpu-baseline --no-enumerate --no-chunk-api $W8_ARGS $xa > $O/w8.json 2> $O/w8.log || { tail -20 $O/w8.log; return 1; }
     line $O/w8.json ;;
   shares)
     mkdir -p $O/shares
