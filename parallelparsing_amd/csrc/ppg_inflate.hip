@@ -813,11 +813,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             uint32_t tl = cw, xr = 0;   // no walk (cn >= 64): the carried word stays
             // lane 0 unconditionally: with no carry (cn == 0) the walk's first token overwrites it
             uint32_t vtin = (uint32_t)llvm_writelane((int)cw, 0, 0);
-#ifdef PPG_V_EXPECT   // A/B (r06): the walk-less round (a carry of >= 64 bytes) laid out off the hot path
+            // the walk-less round (a carry of >= 64 bytes) is rare: laid out off the hot path, the walk
+            // falls through into the emit (r06: -0.7% per 50 GB step, profiles/r06j_ab_layout.json)
             if (__builtin_expect(off < (HOT ? 64u : min(64u, len - pos)), 1)) {
-#else
-            if (off < (HOT ? 64u : min(64u, len - pos))) {
-#endif
                 // the stream bits at bp + lane and bp + 64 + lane (five words per lane from the LDS
                 // ring, read during the previous round's emit); v_alignbit reads only bits [4:0]
                 const uint32_t o = bp + (uint32_t)lane;
@@ -1116,11 +1114,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 hs_emit += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(p_b + lim_r) - h4;
                 st_w0 = 0;
 #endif
-#ifdef PPG_V_LATCH   // A/B (r06): the pipelined loop's latch as the likely edge
-            } while (__builtin_expect(pos < lim_r, 1));
-#else
             } while (pos < lim_r);
-#endif
             finish();
             return lim_r;
         };
