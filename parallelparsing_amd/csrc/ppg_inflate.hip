@@ -67,6 +67,7 @@ struct __attribute__((aligned(16))) InflateLds {
     // (the canonical codes' sorted symbols are in global scratch: see ppg_inflate_kernel)
     uint8_t lens[320];
     uint32_t cen[8];               // newline census: count, previous byte was '\n', PPG_PF_* flags, cap, shift, dst
+    uint16_t dsort[32];            // the distance code's sorted symbols (bit-serial distance codes read them here, r06)
 };
 
 #ifdef PPG_IX_STATS
@@ -82,7 +83,9 @@ __device__ unsigned long long ppg_ixstat[16];
 // token round, summed per wave and added to these totals at the end of each chunk; the launcher
 // prints them (cycles per phase, rounds) after each launch.  Perturbs the schedule (+~10%).
 // [0..7]: the general rounds (one_round); [8..15]: the pipelined rounds (hot_pipe, r05)
-__device__ unsigned long long ppg_stamp_acc[16];
+__device__ unsigned long long ppg_stamp_acc[25];
+// [15..24] (r06): per-wave totals over the whole job -- wave cycles, bit-serial tokens (cycles,
+// count), flushes + census (cycles, count), block headers + table builds (cycles, count), jobs
 #define PPG_STAMP(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #else
 #define PPG_STAMP(t)
@@ -562,8 +565,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
     // 555.2 ms (1 KiB ring, sorted symbols in LDS) -> 533.3; the global sorted symbols alone (1 KiB
     // ring) 565.2, sorting straight into global memory 562.8 / 540.4 (r05zza).
     uint16_t *const lit_sorted = gsort + (size_t)k * PPG_SORT_SLOT;
-    uint16_t *const dst_sorted = lit_sorted + 288;
+    // (r06) the distance code's (30 symbols at most) stay in LDS: no global load per long distance code
+    uint16_t *const dst_sorted = S.dsort;
     uint16_t *const lit_tmp = (uint16_t *)S.dst, *const cl_tmp = (uint16_t *)S.dst, *const dst_tmp = (uint16_t *)S.lens;
+#ifdef PPG_STAMPS
+    const uint64_t tk0 = __builtin_amdgcn_s_memtime();
+    uint64_t sx_spec = 0, sx_nspec = 0, sx_flush = 0, sx_nflush = 0, sx_hdr = 0, sx_nhdr = 0, sx_hp = 0, sx_nhp = 0;
+#endif
     const PpgInflateJob J = jobs[k];
     const uint64_t out_off = J.out_off;
     const uint32_t len = IX ? 0xFFFFFFFFu : (uint32_t)J.out_len;   // < 2^31: ppg_index_validate
@@ -618,7 +626,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
 
     uint32_t pos = 0;                                        // output bytes produced
     uint32_t fl_done = 0;                                    // flushed up to this position
-    uint32_t fl_next = UNIT - (uint32_t)(out_off & (UNIT - 1));   // next global 4 KiB boundary
+    uint32_t fl_next = UNIT - (uint32_t)(out_off % UNIT);   // next global UNIT boundary
     int status = ST_OK, flags = 0, last = 0, in_block = 0;
     Canon clit = {0, 0, 0}, cdst = {0, 0, 0};   // per-lane canonical codes of the current block
     // flush of chunk positions [lo, hi) (never across a UNIT boundary except the plain case)
@@ -675,6 +683,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         fl_done = uni(fl_done);
         fl_next = uni(fl_next);
         status = (int)uni((uint32_t)status);
+#ifdef PPG_STAMPS
+        const uint64_t th0 = __builtin_amdgcn_s_memtime();
+#endif
         rd_refill(r, S.stream, lane);
         last = (int)br_take(r, 1);
         const uint32_t type = br_take(r, 2);
@@ -769,6 +780,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             if (build_table<DB>(S.lens + hlit, (int)hdist, S.dst, &cdst, dst_tmp, TAB_DST, lane, dst_sorted) != 0) { status = ST_DATA_ERROR; break; }
         }
         in_block = 1;
+#ifdef PPG_STAMPS
+        sx_hdr += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(S.lit[lane]) - th0;
+        sx_nhdr++;
+#endif
         asm volatile("s_setprio 0");
         // once per block: tell the compiler the decoder state is wave-uniform (it cannot prove it
         // through the outer loop), so the token rounds keep it in SGPRs with scalar branches
@@ -1065,6 +1080,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 hs_look += h2 - h1;
 #endif
                 finish();
+                if constexpr (!EARLY && !IX) {
+                    // the flush inside the pipelined loop (r06): every byte before pos is in the ring once
+                    // the pending round is finished, and nothing of this round reads the ring yet -- the
+                    // loop no longer ends (and waits for its pending round's far load) at every 1 KiB
+                    // unit (518.3 vs 520.4 ms per 50 GB step, profiles/r06p_ab_inflush.json)
+                    if (pos >= fl_next) {
+                        flush(fl_done, fl_next);
+                        fl_done = fl_next;
+                        fl_next += UNIT;
+                    }
+                }
 #ifdef PPG_STAMPS
                 const uint64_t h3 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(
                                                                        S.ring[(rb0 + p_pos + lane) & RM]);
@@ -1136,13 +1162,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 // 74.17 -> 73.58 / 144.95 -> 143.65 ms, N = 1 unchanged; profiles/r04r/)
                 if (pos < 32768u && pos < limh) {
                     const uint32_t lime = min(limh, 32768u);
+#ifdef PPG_STAMPS
+                    const uint64_t tq0 = __builtin_amdgcn_s_memtime();
+#endif
                     lim_r = hot_pipe(std::true_type{}, lime);
+#ifdef PPG_STAMPS
+                    sx_hp += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)lim_r - tq0;
+                    sx_nhp++;
+#endif
                     spec_ = lim_r == 0u;   // lime > pos >= 0 otherwise
                 }
-                if (!spec_ && pos >= 32768u && pos < limh) {
+                const uint32_t limp = IX ? limh : (len > 322u ? len - 322u : 0u);   // flushes inside the loop
+                if (!spec_ && pos >= 32768u && pos < limp) {
                     // DecompressAll and CreateIndex pass 1 (r04: pass 1 792 -> 671 ms per 50 GB member,
                     // profiles/r04q/)
-                    lim_r = hot_pipe(std::false_type{}, limh);
+#ifdef PPG_STAMPS
+                    const uint64_t tq0 = __builtin_amdgcn_s_memtime();
+#endif
+                    lim_r = hot_pipe(std::false_type{}, limp);
+#ifdef PPG_STAMPS
+                    sx_hp += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)lim_r - tq0;
+                    sx_nhp++;
+#endif
                     spec_ = lim_r == 0u;   // limh > pos >= 0 otherwise
                 }
                 if (!spec_ && pos < lim) {
@@ -1156,23 +1197,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 if (status != ST_OK) break;
             }
             if (pos >= fl_next) {
+#ifdef PPG_STAMPS
+                const uint64_t tf0 = __builtin_amdgcn_s_memtime();
+#endif
                 flush(fl_done, fl_next);
                 fl_done = fl_next;
                 fl_next += UNIT;
+#ifdef PPG_STAMPS
+                sx_flush += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(S.cen[0]) - tf0;
+                sx_nflush++;
+#endif
             }
             if (!spec_) {
                 if (pos < len) continue;   // a flush boundary: more rounds
                 break;
             }
             // ---- one token, bit-serially (long code, end-of-block or invalid) ----
+#ifdef PPG_STAMPS
+            const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+            sx_nspec++;
+#endif
             asm volatile("s_setprio 2");
             rd_seek(r, S.stream, bp, lane);
             rd_refill(r, S.stream, lane);
-            const int sym = canon_decode(r, clit, lit_sorted, lane);
+            // The token the hot rounds stopped at: a litlen code longer than the root (or end-of-block),
+            // or a length whose DISTANCE code is (~60% of them on bench-shape FASTQ): the root tables
+            // first, the sorted symbols (litlen: global scratch; distance: LDS) only for the long code
+            int sym;
+            uint32_t ml = 0;
+            {
+                const uint32_t e = uni(S.lit[(uint32_t)r.bb & ((1u << LBT) - 1)]);
+                if (!(e & 0x80u)) {
+                    const uint32_t L = e & 15u;
+                    br_take(r, L);
+                    if (e & 0x40u) {
+                        ml = ((e >> 16) & 0x1FFu) + br_take(r, ((e >> 8) & 0xFFu) - L);
+                        sym = 257;
+                    } else {
+                        sym = (int)((e >> 17) & 0xFFu);
+                    }
+                } else {
+                    sym = canon_decode(r, clit, lit_sorted, lane);
+                    if (sym > 256 && sym < 286) {
+                        ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
+                        sym = 257;
+                    }
+                }
+            }
 #ifdef PPG_STATS
             if (sym < 256) st_blit++; else if (sym == 256) st_beob++; else st_bmatch++;
 #endif
-            if (sym < 0 || sym >= 286) { status = ST_DATA_ERROR; break; }
+            if (sym < 0 || sym > 257) { status = ST_DATA_ERROR; break; }
             if (sym < 256) {
                 if (lane == 0) S.ring[(rb0 + pos) & RM] = (RingT)((IX ? 0x8000u : 0u) | (uint32_t)sym);
                 pos++;
@@ -1181,11 +1256,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 bp = rd_pos(r);
                 break;
             } else {
-                const uint32_t ml = c_lbase[sym - 257] + br_take(r, c_lext[sym - 257]);
                 rd_refill(r, S.stream, lane);
-                const int dsym = canon_decode(r, cdst, dst_sorted, lane);
-                if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
-                const uint32_t ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
+                uint32_t ds;
+                const uint32_t d = uni(S.dst[(uint32_t)r.bb & ((1u << DB) - 1)]);
+                if (d != ~0u) {
+                    br_take(r, d & 15u);
+                    ds = (d >> 16) + 1u + br_take(r, (d >> 10) & 31u);
+                } else {
+                    const int dsym = canon_decode(r, cdst, dst_sorted, lane);
+                    if (dsym < 0 || dsym >= 30) { status = ST_DATA_ERROR; break; }
+                    ds = c_dbase[dsym] + br_take(r, c_dext[dsym]);
+                }
                 const uint32_t n = min(ml, len - pos);
                 copy_match<RB, IX, RingT, IXM>(S.ring, ob, oa, dict, rb0, pos, ds, n, lane);
                 pos += n;
@@ -1199,6 +1280,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
             st_enter(r, S.stream, bp >> 10, lane);
             W = words(bp);
             asm volatile("s_setprio 0");
+#ifdef PPG_STAMPS
+            sx_spec += __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(W.x4) - ts0;
+#endif
             if (pos >= len) break;
         }
         if (status != ST_OK) break;
@@ -1255,6 +1339,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
         atomicAdd(&ppg_stamp_acc[12], (unsigned long long)hs_words);
         atomicAdd(&ppg_stamp_acc[13], (unsigned long long)hs_emit);
         atomicAdd(&ppg_stamp_acc[14], (unsigned long long)hs_rounds);
+        atomicAdd(&ppg_stamp_acc[15], (unsigned long long)(__builtin_amdgcn_s_memtime() - tk0));
+        atomicAdd(&ppg_stamp_acc[16], (unsigned long long)sx_spec);
+        atomicAdd(&ppg_stamp_acc[17], (unsigned long long)sx_nspec);
+        atomicAdd(&ppg_stamp_acc[18], (unsigned long long)sx_flush);
+        atomicAdd(&ppg_stamp_acc[19], (unsigned long long)sx_nflush);
+        atomicAdd(&ppg_stamp_acc[20], (unsigned long long)sx_hdr);
+        atomicAdd(&ppg_stamp_acc[21], (unsigned long long)sx_nhdr);
+        atomicAdd(&ppg_stamp_acc[22], 1ull);
+        atomicAdd(&ppg_stamp_acc[23], (unsigned long long)sx_hp);
+        atomicAdd(&ppg_stamp_acc[24], (unsigned long long)sx_nhp);
     }
 #endif
     if (lane == 0) {
@@ -1365,10 +1459,10 @@ hipError_t ppg_launch_inflate(hipStream_t s, int ring_bits, int lit_bits, const 
 // diagnostic build: print and reset the per-phase round totals (after the stream drains)
 struct PpgStampPrinter {
     static void dump(hipStream_t s) {
-        unsigned long long h[16] = {0};
+        unsigned long long h[25] = {0};
         if (hipStreamSynchronize(s) != hipSuccess) return;
         if (hipMemcpyFromSymbol(h, HIP_SYMBOL(ppg_stamp_acc), sizeof h) != hipSuccess) return;
-        const unsigned long long z[16] = {0};
+        const unsigned long long z[25] = {0};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(ppg_stamp_acc), z, sizeof z);
         const double r = h[6] ? (double)h[6] : 1.0;
         fprintf(stderr, "PPG_STAMPS rounds %llu far-rounds %llu cycles/round: decode %.1f walk %.1f read %.1f far %.1f "
@@ -1378,6 +1472,19 @@ struct PpgStampPrinter {
         fprintf(stderr, "PPG_STAMPS hot rounds %llu cycles/round: decode %.1f walk %.1f lookup %.1f finish %.1f "
                         "words %.1f emit+tail %.1f total %.1f\n", h[14], h[8] / q, h[9] / q, h[10] / q, h[11] / q,
                 h[12] / q, h[13] / q, (h[8] + h[9] + h[10] + h[11] + h[12] + h[13]) / q);
+        // where a wave's whole job goes (r06): hot rounds, general rounds, bit-serial tokens, flushes,
+        // block headers, the rest (job start, seeks, the last flush, the R-E5 check)
+        const double T = h[15] ? (double)h[15] : 1.0;
+        const double hot = h[8] + h[9] + h[10] + h[11] + h[12] + h[13], gen = h[0] + h[1] + h[2] + h[3] + h[4] + h[5];
+        fprintf(stderr, "PPG_STAMPS jobs %llu wave cycles %.4g: hot rounds %.1f%% general rounds %.1f%% bit-serial tokens "
+                        "%.1f%% (%llu, %.0f cycles each) flushes %.1f%% (%llu, %.0f each) block headers %.1f%% (%llu, %.0f "
+                        "each) other %.1f%%\n", h[22], T, 100 * hot / T, 100 * gen / T, 100 * h[16] / T, h[17],
+                h[16] / (h[17] ? (double)h[17] : 1.0), 100 * h[18] / T, h[19], h[18] / (h[19] ? (double)h[19] : 1.0),
+                100 * h[20] / T, h[21], h[20] / (h[21] ? (double)h[21] : 1.0),
+                100 * (T - hot - gen - h[16] - h[18] - h[20]) / T);
+        fprintf(stderr, "PPG_STAMPS pipelined-loop calls %llu: %.1f%% of wave cycles inside them, %.0f cycles per call "
+                        "outside their rounds (entry, the pending round's finish, exit)\n", h[24], 100 * h[23] / T,
+                (h[23] - hot) / (h[24] ? (double)h[24] : 1.0));
     }
 };
 #endif
