@@ -1066,10 +1066,10 @@ constexpr int kSlots = 16;    // pinned staging slots at most (IngestState::nslo
 constexpr int kPieces = 3;   // device piece slots: one finishing, one decoding, one filling
 
 struct IngestState {
-    // staging shape, fixed when the state is made: 4 slots of 128 MB on one copy stream by default;
+    // staging shape, fixed when the state is made: 4 slots of a quarter piece (<= 512 MiB) on one copy stream by default;
     // PPG_INGEST_SLOTS / PPG_INGEST_SLOT_MB / PPG_INGEST_COPY_STREAMS (1-2) for A/B runs (tools/ingest_probe.py)
     int nslots = 4, ncs = 1;
-    int64_t slot_bytes = (int64_t)128 << 20;
+    int64_t slot_bytes = (int64_t)512 << 20;
     PinnedBuf slot[kSlots];       // pinned host staging, streamed through round-robin
     hipEvent_t slot_ev[kSlots] = {};
     hipStream_t cs2 = nullptr;    // a second copy stream (ncs == 2): odd slots
@@ -1171,7 +1171,11 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
             return e ? std::min(hi, std::max(lo, (int64_t)strtoll(e, nullptr, 10))) : d;
         };
         st->nslots = (int)env_int("PPG_INGEST_SLOTS", 4, 2, kSlots);
-        st->slot_bytes = env_int("PPG_INGEST_SLOT_MB", 128, 8, 1024) << 20;
+        // slots of a quarter piece, at most 512 MiB (r06: 4 x 512 MiB vs 4 x 128 MiB pinned slots,
+        // 1.02-1.05 vs 1.16-1.24 s per 50 GB member in one process: fewer, longer preads and copies;
+        // 1 GiB slots no better -- profiles/r06v_ingest_slots.json); sized by the first call
+        const int64_t auto_mb = std::min<int64_t>(512, std::max<int64_t>(8, (maxlen / 4 + (1 << 20) - 1) >> 20));
+        st->slot_bytes = env_int("PPG_INGEST_SLOT_MB", auto_mb, 8, 1024) << 20;
         st->ncs = (int)env_int("PPG_INGEST_COPY_STREAMS", 1, 1, 2);
         // the copy stream at the greatest priority, i.e. on a hardware queue of its own: a stream
         // sharing a queue with a decode stream runs in order behind its kernels, and the piece copies
@@ -1266,7 +1270,7 @@ int ppg_file_decompress_all(ppg_ctx *ctx, const ppg_index *ix, const char *gz_pa
                 rcp = PPG_DEVICE_ERROR;
             if (verbose)
                 fprintf(stderr, "[ingest] piece %zu: %.1f MB read+copy at %.1f ms in %.1f ms (pread %.1f ms, slowest "
-                        "128 MB %.1f ms; waiting for pinned slots %.1f ms; copy enqueues %.1f ms)\n", k, len / 1e6, t1,
+                        "slot %.1f ms; waiting for pinned slots %.1f ms; copy enqueues %.1f ms)\n", k, len / 1e6, t1,
                         now_ms() - t1, read_ms, slow_ms, wait_ms, enq_ms);
             std::lock_guard<std::mutex> lk(mu);
             if (rcp != PPG_OK) prod_rc = rcp;

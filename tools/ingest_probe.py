@@ -127,6 +127,37 @@ def main():
             torch.cuda.synchronize()
             best = max(best, n / (time.perf_counter() - t) / 1e9)
         res["pcie_h2d_GBps"] = best
+        # the ingest's copy shapes: 128 / 512 MiB copies back to back from rotating pinned slots
+        for mb in (128, 512):
+            m = mb << 20
+            best = 0.0
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for i in range(n // m):
+                    d[i * m:(i + 1) * m].copy_(h[i * m:(i + 1) * m], non_blocking=True)
+                torch.cuda.synchronize()
+                best = max(best, n / (time.perf_counter() - t) / 1e9)
+            res[f"pcie_h2d_GBps_{mb}MiB_copies"] = best
+        # NUMA: the GPU's node, the pinned buffer's pages, the CPUs this process may run on
+        try:
+            nodes = {}
+            for c in sorted(os.listdir("/sys/class/drm")):
+                f = f"/sys/class/drm/{c}/device/numa_node"
+                if c.startswith("card") and "-" not in c and os.path.exists(f):
+                    nodes[c] = open(f).read().strip()
+            res["drm_numa_nodes"] = nodes
+            res["cpus_allowed"] = len(os.sched_getaffinity(0))
+            libc = C.CDLL(None, use_errno=True)
+            libc.syscall.restype = C.c_long
+            step = 256 << 20
+            offs = list(range(0, n, step))
+            pages = (C.c_void_p * len(offs))(*[h.data_ptr() + o for o in offs])
+            status = (C.c_int * len(offs))()
+            rc = libc.syscall(SYS_move_pages, 0, C.c_ulong(len(offs)), pages, None, status, 0)
+            res["pinned_page_nodes"] = list(status) if rc == 0 else f"rc {rc}"
+        except OSError as e:
+            res["numa_error"] = str(e)
     finally:
         if os.path.exists(path):
             os.remove(path)
