@@ -860,7 +860,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                     X = off << 8;
                     asm volatile("s_setprio 2");
                     walk2_asm(vta, vtb, vtin, X, tl, half);
-                    asm volatile("s_setprio 1");
+                    // the HOT rounds keep priority 2 through the token lookup (hot_pipe), then 0
+                    if constexpr (!HOT) asm volatile("s_setprio 1");
                     off = (X >> 8) & 511u;
                 } else {
                     const uint32_t cl = 64u - (len - pos);   // off < len - pos  <=>  off + cl < 64
@@ -1075,6 +1076,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(80), amdgpu_wave
                 uint32_t sj4;
                 asm("v_mad_i32_i24 %0, %1, -4, %2" : "=v"(sj4) : "v"((uint32_t)__builtin_clzll(mo & lanes_le)), "s"(252u));
                 const uint32_t inf = bperm(sj4, R.vtin);
+                // r06: the walk's priority 2 held through the token lookup, then 0 for the rest of the
+                // round (finish, flush, stream words, emit) -- was 1 from the walk's end to the round's
+                // tail: 520.0 -> 518.4 / 515.8 -> 513.8 ms per 50 GB step on two boxes
+                // (profiles/r06zj_ab_prio_place2.json, r06zk_ab_prio_place3.json; the tail's own
+                // s_setprio 0, now redundant, stays: without it 522.6)
+                asm volatile("s_setprio 0");
 #ifdef PPG_STAMPS
                 const uint64_t h2 = __builtin_amdgcn_s_memtime() + 0 * (uint64_t)__builtin_amdgcn_readfirstlane(inf);
                 hs_look += h2 - h1;
